@@ -1,0 +1,116 @@
+/*
+ * kmerpapa_hip.h -- C-ABI of the MI355X lattice-DP engine (libkmerpapa_hip.so).
+ *
+ * Plain C types only (no torch, no HIP types).  Every call returns KP_OK (0) or a
+ * negative KP_E_* code; kp_last_error() gives the thread's last message.  Host buffers
+ * are owned by the caller and only read (or written, for outputs) during the call.
+ * Device memory is owned by the plan and cached across passes.
+ *
+ * What each entry point replaces in the reference (BesenbacherLab/kmerPaPa v0.2.4;
+ * "CV" = src/kmerpapa/algorithms/bottum_up_array_penalty_plus_pseudo_CV.py,
+ *  "Fit" = src/kmerpapa/algorithms/bottum_up_array_w_numba.py):
+ *
+ *   kp_plan_create   per-pattern globals and tables: CV :82-122, Fit :68-92;
+ *                    pattern_utils.py pattern_max :587, get_cum_genpat_pos_level :237,
+ *                    subpatterns_level_ord_np :513 (level order)
+ *   kp_set_counts    level-0 rows of M_mem/U_mem written by
+ *                    CV_tools.make_all_folds_contextD_patterns (CV :130) or by the Fit
+ *                    level-0 loop (Fit :106-114), plus every aggregated row
+ *                    (first-pair sums, CV :52-55 / Fit :50-53)
+ *   kp_pass          the level sweep CV :143-157 (score_test_folds :15-20 and
+ *                    handle_pattern :26-78 for every cell) and its root read-out
+ *                    :158-163; with fold = -1 the Fit sweep Fit :106-120
+ *   kp_fit_leaves    backtrack(gen_pat, ...) Fit :17-24, 121
+ */
+#ifndef KMERPAPA_HIP_H
+#define KMERPAPA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KP_OK 0
+#define KP_E_ARG (-1)     /* bad argument (pattern, sizes, lane count)            */
+#define KP_E_NOMEM (-2)   /* lattice x lanes does not fit device memory             */
+#define KP_E_HIP (-3)     /* HIP runtime / launch failure                           */
+#define KP_E_STATE (-4)   /* call order violated (e.g. kp_pass before kp_set_counts) */
+#define KP_E_PARITY (-5)  /* internal consistency check failed (argmin tree broken) */
+
+#define KP_GROUP_MAX_LANES 8
+
+typedef struct kp_ctx kp_ctx;
+typedef struct kp_plan kp_plan;
+
+/* One (pseudo-count alpha, fold) group: n_lanes penalties share the fold's counts.
+ * fold in [0, nf) = cross-validation on that fold (train = all other folds);
+ * fold = -1      = fit on all data (the Fit module's DP). */
+typedef struct {
+    int32_t fold;
+    int32_t n_lanes;
+    double alpha;
+    double beta;
+    double penalty[KP_GROUP_MAX_LANES];
+} kp_group;
+
+typedef struct {
+    uint64_t npat;        /* lattice cells = pattern_max(gen_pat)                  */
+    uint64_t nblocks;     /* LDS blocks                                            */
+    uint64_t n_kmers;     /* k-mers matching gen_pat                               */
+    uint32_t block;       /* cells per block (low positions)                       */
+    uint32_t block_pad;   /* row stride of a block lane                            */
+    int32_t k, low_positions, max_level, high_levels;
+    double pairs_total;   /* split pairs summed over all cells (SURVEY 8d "P")    */
+    double pairs_high;    /* ... of which at high (gathered) positions             */
+    uint64_t bytes_per_lane; /* device bytes per lane (train f32 + argmin u8)     */
+} kp_plan_info;
+
+typedef struct {
+    double dp_ms;         /* device time of the DP sweep kernels (HIP events)      */
+    double backtrack_ms;  /* device time of the backtrack kernel                   */
+    double total_ms;      /* host wall time of the whole kp_pass call              */
+    uint64_t units;       /* cells x lanes scored in the pass                      */
+    uint64_t dp_launches; /* kernel launches of the sweep                          */
+    double alg_bytes;     /* algorithmic bytes of the pass (SURVEY 8d definition)  */
+    double gather_bytes;  /* bytes the sweep gathers from HBM/L2 (high splits)     */
+} kp_pass_stats;
+
+const char *kp_last_error(void);
+int kp_device_count(int *n);
+
+int kp_create(int device, kp_ctx **out);
+void kp_destroy(kp_ctx *ctx);
+/* free / total device memory of the context's GPU (bytes) */
+int kp_device_mem(kp_ctx *ctx, uint64_t *free_bytes, uint64_t *total_bytes);
+
+/* max_block = 0 -> default LDS block budget (4096 cells). */
+int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan **out);
+void kp_plan_destroy(kp_plan *plan);
+int kp_plan_get_info(const kp_plan *plan, kp_plan_info *out);
+
+/* Upload fold counts of every k-mer: M, U are [n_kmers][nf] arrays of itype_bytes (4 or
+ * 8) unsigned integers, k-mers in KmerEnumeration order (position 0 fastest, nucleotide
+ * index = position in code[g]).  Builds the per-block k-mer-low count tables. */
+int kp_set_counts(kp_plan *plan, const void *M, const void *U, uint64_t n_kmers, int nf, int itype_bytes);
+
+/* One DP sweep of every lane of every group over the whole lattice.
+ * Lanes are numbered group-major; per lane the outputs are the root's train score
+ * (f32, as stored by the reference), the root's test -2LL (CV) and the number of
+ * patterns of the optimal partition. */
+int kp_pass(kp_plan *plan, const kp_group *groups, int n_groups, float *root_train, float *root_test,
+            uint64_t *n_leaves);
+int kp_last_pass_stats(const kp_plan *plan, kp_pass_stats *out);
+
+/* Leaves (cell indices) of lane `lane` of the last pass, in the reference's backtrack
+ * order.  cap = capacity of `leaves`; *n_out = number of leaves. */
+int kp_fit_leaves(kp_plan *plan, uint32_t lane, uint64_t *leaves, uint64_t cap, uint64_t *n_out);
+
+/* Debug / parity: copy one lane's train scores and argmin codes, in cell-index order
+ * ([npat] each; either pointer may be NULL). */
+int kp_dump_lane(kp_plan *plan, uint32_t lane, float *score, uint8_t *code);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

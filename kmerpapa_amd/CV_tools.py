@@ -1,0 +1,106 @@
+"""Cross-validation fold splitting (host side, numpy legacy RNG).
+
+Same API and, crucially, the same random stream as the reference module
+``kmerpapa.CV_tools`` (src/kmerpapa/CV_tools.py): every fold is a multivariate
+hypergeometric draw made colour by colour with ``RandomState.hypergeometric``, in the
+order the reference walks the colours, so a given seed yields bit-identical folds.
+
+The device path never sees the ``[npat, nf]`` arrays of the reference (a 9-mer lattice
+has 7.7e9 rows): :func:`fold_tables` returns only the per-k-mer fold counts, which the
+C-ABI uploads (``kp_set_counts``).
+"""
+import numpy as np
+
+from .pattern_utils import PatternEnumeration, matches
+
+
+def sample(m, colors, itype, prng):
+    """Draw ``m`` balls from an urn with ``colors[i]`` balls of colour i (ref CV_tools.py:5-27).
+
+    Colours are visited in order; colour i gets ``hypergeometric(colors[i], rest, m_left)``
+    where ``rest`` counts the balls of all later colours; the walk stops once nothing is
+    left to draw and the last colour takes the remainder.
+    """
+    colors = np.asarray(colors)
+    n = len(colors)
+    tail = np.cumsum(colors[::-1])[::-1]  # tail[i] = balls in colours i..n-1
+    out = np.zeros(n, dtype=itype)
+    left = int(m)
+    draw = prng.hypergeometric
+    for i in range(n - 1):
+        if left < 1:
+            break
+        got = int(draw(int(colors[i]), int(tail[i + 1]), left))
+        out[i] = got
+        left -= got
+    out[-1] = left
+    return out
+
+
+def _split_colors(colors, n_folds, itype, prng):
+    """Folds 0..nf-2 by :func:`sample`, the last fold takes what is left (ref :53-57)."""
+    colors = np.array(colors, dtype=itype, copy=True)
+    per_fold = int(colors.sum()) // n_folds
+    folds = np.empty((len(colors), n_folds), dtype=itype)
+    for f in range(n_folds - 1):
+        s = sample(per_fold, colors, itype, prng)
+        folds[:, f] = s
+        colors -= s
+    folds[:, n_folds - 1] = colors
+    return folds
+
+
+def fold_tables(contextD, n_folds, prng, itype=np.uint64):
+    """Fold counts per k-mer, in sorted-context order.
+
+    Returns ``(contexts, M, U)`` with ``M, U`` of shape ``[n_kmers, n_folds]``: exactly the
+    level-0 rows :func:`make_all_folds_contextD_patterns` scatters into ``M_mem``/``U_mem``.
+    """
+    contexts = sorted(contextD)
+    nk = len(contexts)
+    colors = np.empty(2 * nk, dtype=itype)
+    for i, c in enumerate(contexts):
+        nm, nu = contextD[c]
+        colors[i] = nm
+        colors[nk + i] = nu
+    folds = _split_colors(colors, n_folds, itype, prng)
+    return contexts, folds[:nk], folds[nk:]
+
+
+def make_all_folds_contextD_patterns(contextD, U_mem, M_mem, general_pattern, prng, itype=np.uint64):
+    """Fill the k-mer rows of ``M_mem``/``U_mem`` ``[npat, nf]`` with fold counts (ref :30-62)."""
+    PE = PatternEnumeration(general_pattern)
+    contexts, M, U = fold_tables(contextD, U_mem.shape[1], prng, itype)
+    for i, c in enumerate(contexts):
+        row = PE.pattern2num(c)
+        M_mem[row] = M[i]
+        U_mem[row] = U[i]
+
+
+def make_all_folds_contextD_kmers(contextD, U_mem, M_mem, general_pattern, prng):
+    """Fold counts for every k-mer of ``general_pattern`` in :func:`matches` order (ref :65-96)."""
+    contexts = list(matches(general_pattern))
+    nk = len(contexts)
+    colors = np.zeros(2 * nk, dtype=np.uint64)
+    for i, c in enumerate(contexts):
+        nm, nu = contextD[c]
+        colors[i] = nm
+        colors[nk + i] = nu
+    folds = _split_colors(colors, U_mem.shape[1], np.uint64, prng)
+    M_mem[:nk] = folds[:nk]
+    U_mem[:nk] = folds[nk:]
+
+
+def make_all_folds(kmer_table, n_folds, n_repeats, prng):
+    """Split a count table into ``n_folds`` folds, ``n_repeats`` times (ref :124-147).
+
+    Returns an array of shape ``(n_repeats, n_folds) + kmer_table.shape``.
+    """
+    kmer_table = np.asarray(kmer_table)
+    itype = kmer_table.dtype
+    out = np.zeros((n_repeats, n_folds) + kmer_table.shape, dtype=itype)
+    for r in range(n_repeats):
+        folds = _split_colors(kmer_table.reshape(-1), n_folds, itype, prng)
+        for f in range(n_folds):
+            out[r, f] = folds[:, f].reshape(kmer_table.shape)
+    return out

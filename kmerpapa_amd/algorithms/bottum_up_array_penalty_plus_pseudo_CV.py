@@ -1,0 +1,140 @@
+"""Cross-validated penalized-likelihood pattern partition -- drop-in for the reference's
+``kmerpapa.algorithms.bottum_up_array_penalty_plus_pseudo_CV`` (v0.2.4).
+
+``pattern_partition_bottom_up(gen_pat, contextD, alphas, args, nmut, nunmut, penalties,
+index_mut=0)`` keeps the reference's signature, return value ``(best_alpha,
+best_penalty, best_test_loss)``, stderr lines and CVfile rows (CV module :81-177).
+
+What moved to the GPU: the whole level sweep (CV :143-157, ``handle_pattern`` :26-78 and
+``score_test_folds`` :15-20) for every (alpha, penalty, fold) at once -- one lane per
+(penalty, fold), lanes of one (alpha, fold) sharing counts -- and the root read-out
+(:158-163).  What stays on the host, bit-identical to the reference: the fold split
+(``RandomState.hypergeometric`` stream, CV :124-130), fold totals and betas (:134-141),
+the numpy<2 float64 sum of the root test values (:159, :171), the strict-"<" selection
+in alpha-major order (:165-177).
+"""
+import sys
+
+import numpy as np
+
+from .. import engine
+from ..CV_tools import fold_tables
+from ..pattern_utils import code, generality, pattern_level, perm_code
+from ..score_utils import get_betas
+
+
+def _itype(nmut, nunmut):
+    """uint32 unless the totals need 64 bits (CV :94-97)."""
+    return np.uint64 if nmut + nunmut > np.iinfo(np.uint32).max else np.uint32
+
+
+def _cells_per_kmer(gen_pat):
+    """For every k-mer (KmerEnumeration order): number of lattice cells that contain it."""
+    mult = np.ones(1, dtype=np.uint64)
+    for g in gen_pat:
+        per = np.array([sum(1 for x in perm_code[g] if nuc in code[x]) for nuc in code[g]], dtype=np.uint64)
+        mult = (per[:, None] * mult[None, :]).reshape(-1)  # position 0 fastest
+    return mult
+
+
+def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, itype, devices=None, verbose=0,
+             max_block=0, run_groups=None):
+    """Root train/test values of every (iteration, alpha, penalty, fold).
+
+    Returns a dict with arrays ``train``/``test`` of shape
+    ``[iterations, n_alpha, n_penalty, nfolds]`` (float32) and ``betas``
+    ``[iterations, n_alpha, nfolds]``.  ``run_groups`` defaults to the GPU engine.
+    """
+    run_groups = run_groups or engine.run_groups
+    prng = np.random.RandomState(seed)
+    na, nc = len(alphas), len(penalties)
+    train = np.zeros((iterations, na, nc, nfolds), np.float32)
+    test = np.zeros((iterations, na, nc, nfolds), np.float32)
+    betas_all = np.zeros((iterations, na, nfolds))
+    n_kmers = generality(gen_pat)
+    mult = None
+    prevM = prevU = None
+    for it in range(iterations):
+        if verbose > 0 and iterations > 1:
+            print('CV Iteration', it, file=sys.stderr)
+        contexts, Mf, Uf = fold_tables(contextD, nfolds, prng, itype)
+        if verbose > 0:
+            print('CV sampling DONE', file=sys.stderr)
+        Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, n_kmers, itype)
+        # fold totals = column sums of M_mem over ALL rows (CV :134-137).  From the
+        # second iteration on, the aggregated rows still hold the previous iteration's
+        # sums: every k-mer count of the previous split appears once per containing
+        # cell other than the k-mer itself.  Reproduced as the reference computes it.
+        M_sum = Mk.sum(axis=0, dtype=np.uint64)
+        U_sum = Uk.sum(axis=0, dtype=np.uint64)
+        if prevM is not None:
+            if mult is None:
+                mult = _cells_per_kmer(gen_pat) - np.uint64(1)
+            M_sum = M_sum + (prevM.astype(np.uint64) * mult[:, None]).sum(axis=0, dtype=np.uint64)
+            U_sum = U_sum + (prevU.astype(np.uint64) * mult[:, None]).sum(axis=0, dtype=np.uint64)
+        M_train = M_sum.sum() - M_sum
+        U_train = U_sum.sum() - U_sum
+        groups, where = [], []
+        for a_i, alpha in enumerate(alphas):
+            betas = get_betas(alpha, M_train, U_train)
+            betas_all[it, a_i] = betas
+            for f in range(nfolds):
+                for c0 in range(0, nc, engine.MAX_GROUP_LANES):
+                    chunk = list(penalties[c0:c0 + engine.MAX_GROUP_LANES])
+                    groups.append((f, alpha, float(betas[f]), chunk))
+                    where.extend((a_i, c0 + j, f) for j in range(len(chunk)))
+        rt, re, _ = run_groups(gen_pat, Mk, Uk, groups, devices=devices, max_block=max_block)
+        for lane, (a_i, p_i, f) in enumerate(where):
+            train[it, a_i, p_i, f] = rt[lane]
+            test[it, a_i, p_i, f] = re[lane]
+        prevM, prevU = Mk, Uk
+        if verbose > 0:
+            _report(gen_pat, alphas, penalties, it, test[it], verbose)
+    return {"train": train, "test": test, "betas": betas_all}
+
+
+def _report(gen_pat, alphas, penalties, it, test, verbosity):
+    """stderr lines of one iteration, in the reference's pass order (CV :153-161)."""
+    level = pattern_level(gen_pat)
+    for a_i, alpha in enumerate(alphas):
+        for p_i, penalty in enumerate(penalties):
+            if verbosity > 1:
+                for lv in range(1, level + 1):
+                    print(f'level {lv} of {level}', file=sys.stderr)
+            roots = test[a_i, p_i]
+            print(f'CV on k={len(gen_pat)} alpha={alpha} penalty={penalty} i={it} test_LL={_f64_sum(roots)}',
+                  file=sys.stderr)
+            if verbosity > 1:
+                print(f'test LL for each fold: {roots}', file=sys.stderr)
+
+
+def _f64_sum(values):
+    """sum() of float32 scalars under the reference's pinned numpy<2 (float64 accumulation)."""
+    acc = 0.0
+    for v in values:
+        acc += float(v)
+    return acc
+
+
+def pattern_partition_bottom_up(gen_pat, contextD, alphas, args, nmut, nunmut, penalties, index_mut=0):
+    """Grid CV over (alpha, penalty); returns ``(best_alpha, best_penalty, best_test_loss)`` (CV :81-177)."""
+    nf = args.nfolds
+    nit = args.iterations
+    verbosity = getattr(args, "verbosity", 0) or 0
+    itype = _itype(nmut, nunmut)
+    if index_mut != 0:
+        contextD = {k: (v[index_mut], v[-1]) for k, v in contextD.items()}
+    res = cv_roots(gen_pat, contextD, list(alphas), list(penalties), nf, args.seed, nit, itype,
+                   devices=engine.visible_devices(), verbose=verbosity)
+    best_test_loss = 1e100
+    best_values = (None, None)
+    for a_i, alpha in enumerate(alphas):
+        for p_i, penalty in enumerate(penalties):
+            vals = [res["test"][it, a_i, p_i, f] for it in range(nit) for f in range(nf)]
+            test = _f64_sum(vals) / nit
+            if args.CVfile is not None:
+                print(len(gen_pat), alpha, penalty, test, file=args.CVfile)
+            if test < best_test_loss:
+                best_values = (alpha, penalty)
+                best_test_loss = test
+    return best_values[0], best_values[1], best_test_loss

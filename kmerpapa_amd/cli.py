@@ -1,0 +1,207 @@
+"""Command line front-end -- same flags, flow and output as the reference's
+``kmerpapa.cli`` (src/kmerpapa/cli.py:16-318, v0.2.4).
+
+The flow: read counts -> penalty presets -> general pattern (LCA) + zero fill ->
+(optional) grid cross-validation on the GPU -> final fit on the GPU -> partition table.
+Out of scope in this build: ``--greedy``, ``--greedyCV``, ``--BayesOpt``
+and ``--score all_kmers``; they are accepted by the parser and rejected with a message.
+"""
+import argparse
+import sys
+from math import log
+
+from . import __version__
+from .algorithms import bottum_up_array_penalty_plus_pseudo_CV, bottum_up_array_w_numba
+from .io_utils import downsize_contextD, read_input
+from .papa import Pattern
+from .pattern_utils import LCA_pattern_of_kmers, get_M_U, matches
+from .score_utils import get_loss
+
+
+def get_parser():
+    """The argument parser (flags as cli.py:16-115)."""
+    p = argparse.ArgumentParser(prog="kmerpapa",
+                                description="Finds optimal k-mer pattern partition in fx. mutation data")
+    p.add_argument("-p", "--positive", type=argparse.FileType("r"),
+                   help="File with k-mer counts in positive set")
+    p.add_argument("-n", "--negative", type=argparse.FileType("r"),
+                   help="File with k-mer counts in negative set. If the negative set is created with a larger k "
+                        "than the positive set then the k-mers will be collapsed so that they have the same length.")
+    p.add_argument("-b", "--background", type=argparse.FileType("r"),
+                   help="File with k-mer counts in backgound set (includes both positive and negative regions). "
+                        "If the background set is created with a larger k than the positive set then the k-mers "
+                        "will be collapsed so that they have the same length.")
+    p.add_argument("-j", "--joint_context_counts", type=argparse.FileType("r"),
+                   help="File with k-mer counts in positive set and background set. This option can be used "
+                        "instead of having positive and negative counts in seperate files.")
+    p.add_argument("-o", "--output", type=argparse.FileType("w"), default="-", metavar="PATH",
+                   help="Output file (default: standard output)")
+    p.add_argument("-f", "--CVfile", type=argparse.FileType("w"),
+                   help="File with training and test likelihood values from cross validation.")
+    p.add_argument("--verbosity", type=int, default=1,
+                   help="Amount of info printed to stderr during execution. 0:silent, 1:default, 2:verbose")
+    p.add_argument("--CV_only", action="store_true",
+                   help="Only run crossvalidation. Do not run on whole data set using best values afterwards.")
+    p.add_argument("--greedy", action="store_true",
+                   help="Use a fast greedy heuristic (not available in this build).")
+    p.add_argument("--BayesOpt", action="store_true",
+                   help="Bayesian Optimization of pseudo_count and penalty (not available in this build).")
+    p.add_argument("--greedyCV", action="store_true",
+                   help="Greedy heuristic during CV (not available in this build).")
+    p.add_argument("-l", "--long_output", action="store_true", help="Print all k-mers in output format.")
+    p.add_argument("-s", "--super_pattern", type=str,
+                   help="If a super-pattern is provided the program will only consider k-mers that match that "
+                        "pattern.")
+    p.add_argument("--score", type=str, default="penalty_and_pseudo",
+                   choices=["penalty_and_pseudo", "all_kmers", "BIC", "AIC", "HQ", "LL"],
+                   help='Type of score function. Default is "penalty_and_pseudo". '
+                        '"all_kmers" will calculate a rate for each k-mer.')
+    p.add_argument("-N", "--nfolds", type=int, metavar="N",
+                   help="Perform cross validation with N folds. If more than one value of pseudo_count and "
+                        "penalty is given then default is 2. Otherwise default is not to run cross validation "
+                        "if --nfolds option is not set.")
+    p.add_argument("-i", "--iterations", type=int, default=1, metavar="i", help="Repeat cross validation i times")
+    p.add_argument("-a", "--pseudo_counts", type=float, metavar="a", nargs="+", default=[0.8],
+                   help="Different pseudo count (alpha) values to test using cross validation")
+    p.add_argument("-c", "--penalty_values", type=float, metavar="c", nargs="+",
+                   help="Different penalty values to test using cross validation. If no value is set for the "
+                        "default scoring function then log(#k-mers) will be used.")
+    p.add_argument("--test_smaller_k", action="store_true",
+                   help="By standard k is the width of the k-mers in the input data. If this option is supplied "
+                        "it will test all odd numbern up to the width using CV and use the best.")
+    p.add_argument("--seed", type=int, help="seed for numpy.random")
+    p.add_argument("-V", "--version", action="store_true", help="Print version number and return")
+    return p
+
+
+def _out_of_scope(args):
+    if args.greedy or args.greedyCV or args.BayesOpt:
+        return "--greedy / --greedyCV / --BayesOpt"
+    if args.score == "all_kmers":
+        return "--score all_kmers"
+    return None
+
+
+def main(args=None):
+    """Run the program (cli.py:118-318).  Returns an exit code."""
+    parser = get_parser()
+    args = parser.parse_args(args=args)
+    if args.version:
+        print("version:", __version__)
+        print()
+        return 0
+    missing = _out_of_scope(args)
+    if missing:
+        print(f"{missing} is not part of this MI355X build (only the optimal lattice DP is).", file=sys.stderr)
+        return 2
+    super_pattern = Pattern(args.super_pattern) if args.super_pattern is not None else None
+    try:
+        contextD, n_unmut, n_mut = read_input(args, super_pattern)
+    except Exception as e:  # the reference prints help and returns 0 on bad input (cli.py:144-153)
+        parser.print_help()
+        print("=" * 80, file=sys.stderr)
+        print("input error:", file=sys.stderr)
+        print(e, file=sys.stderr)
+        print("=" * 80, file=sys.stderr)
+        return 0
+    verbose = args.verbosity > 0
+    if verbose:
+        print(f"Input data read. {n_mut} positive k-mers and {n_unmut} negative k-mers", file=sys.stderr)
+
+    if args.penalty_values is not None:
+        assert args.score == "penalty_and_pseudo", \
+            f"you cannot specify penalty values when using the {args.score} score function"
+    else:
+        presets = {"BIC": lambda: [log(n_mut)], "AIC": lambda: [2.0], "HQ": lambda: [log(log(n_mut))],
+                   "LL": lambda: [0.0]}
+        if args.score in presets:
+            args.penalty_values = presets[args.score]()
+        elif args.score == "penalty_and_pseudo":
+            args.penalty_values = [log(len(contextD))]  # before zero fill (cli.py:171-175)
+            if verbose:
+                print(f"penalty values not set. Using {args.penalty_values[0]}", file=sys.stderr)
+        else:
+            raise AssertionError(f"illegal score option {args.score}")
+
+    gen_pat = LCA_pattern_of_kmers(list(contextD.keys()))
+    if args.super_pattern is not None:
+        assert gen_pat == args.super_pattern
+    for context in matches(gen_pat):
+        if context not in contextD:
+            contextD[context] = (0, 0)
+    if verbose:
+        print(f"General pattern: {gen_pat}", file=sys.stderr)
+    if args.CVfile is not None:
+        print("k alpha P LL_test", file=args.CVfile)
+
+    best_alpha = best_penalty = best_k = None
+    ks = range(len(gen_pat), 1, -2) if args.test_smaller_k else [len(gen_pat)]
+    this_contextD, this_gen_pat = contextD, gen_pat
+    best_score = 1e100
+    if args.nfolds is None and (len(ks) > 1 or len(args.pseudo_counts) > 1 or len(args.penalty_values) > 1
+                                or args.CV_only):
+        args.nfolds = 2
+    if args.nfolds is not None and args.nfolds > 1:
+        for k in ks:
+            if verbose:
+                print(f"Running {args.nfolds}-fold cross validation on {k}-mers", file=sys.stderr)
+            if k != len(this_gen_pat):
+                this_contextD, this_gen_pat = downsize_contextD(this_contextD, this_gen_pat, k)
+                this_contextD = {key: tuple(v) for key, v in this_contextD.items()}
+            this_alpha, this_penalty, test_score = bottum_up_array_penalty_plus_pseudo_CV.pattern_partition_bottom_up(
+                this_gen_pat, this_contextD, args.pseudo_counts, args, n_mut, n_unmut, args.penalty_values)
+            if test_score < best_score:
+                best_score, best_k, best_alpha, best_penalty = test_score, k, this_alpha, this_penalty
+        if verbose:
+            print(f"CV DONE. best_k={best_k}, best_alpha={best_alpha}, best_penalty={best_penalty}, "
+                  f"best_test_LL={best_score}", file=sys.stderr)
+    if args.CVfile is not None:
+        args.CVfile.close()
+    if args.CV_only:
+        return 0
+
+    if best_alpha is None:
+        assert len(args.pseudo_counts) == 1
+        best_alpha = args.pseudo_counts[0]
+    if best_penalty is None:
+        assert len(args.penalty_values) == 1
+        best_penalty = args.penalty_values[0]
+    if best_k is None:
+        best_k = len(gen_pat)
+    if best_k != len(gen_pat):
+        contextD, gen_pat = downsize_contextD(contextD, gen_pat, best_k)
+        contextD = {key: tuple(v) for key, v in contextD.items()}
+
+    my = n_mut / (n_mut + n_unmut)
+    best_beta = (best_alpha * (1.0 - my)) / my
+    if verbose:
+        print(f"Training on whole data set with k={best_k} alpha={best_alpha} penalty={best_penalty}",
+              file=sys.stderr)
+    best_score, M, U, names = bottum_up_array_w_numba.pattern_partition_bottom_up(
+        gen_pat, contextD, best_alpha, best_beta, best_penalty, args, n_mut, n_unmut)
+
+    counts = [get_M_U(pat, contextD) for pat in names]
+    # partition sanity checks of the reference (cli.py:289-292)
+    assert M == n_mut
+    assert U == n_unmut
+    assert n_mut == sum(x[0] for x in counts)
+    assert n_unmut == sum(x[1] for x in counts)
+    if verbose:
+        print(f"Optimal k-mer pattern partition contains {len(names)} patterns.", file=sys.stderr)
+        print(f"loss={best_score}", file=sys.stderr)
+        print(f"LL={get_loss(counts, best_alpha, best_beta)}", file=sys.stderr)
+
+    out = args.output
+    if args.long_output:
+        print("context", "c_neg", "c_pos", "c_rate", "pattern", "p_neg", "p_pos", "p_rate", file=out)
+    else:
+        print("pattern", "p_neg", "p_pos", "p_rate", file=out)
+    for pat, (Mp, Up) in zip(names, counts):
+        p = (Mp + best_alpha) / (Mp + Up + best_alpha + best_beta)
+        if args.long_output:
+            for context in matches(pat):
+                nm, ns = contextD[context]
+                print(context, ns, nm, float(nm) / (nm + ns), pat, Up, Mp, p, file=out)
+        else:
+            print(pat, Up, Mp, p, file=out)
+    return 0

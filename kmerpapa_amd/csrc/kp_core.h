@@ -1,0 +1,332 @@
+// kp_core.h -- data layout and per-item arithmetic of the blocked lattice DP.
+//
+// Shared by the gfx950 kernels (kp_hip.hip) and by the host-side test emulator
+// (tests/emu/kp_emu.hip), both compiled by hipcc.  Everything here is plain
+// __host__ __device__ code: no launches, no LDS declarations.
+//
+// The recurrence is the reference's (src/kmerpapa/algorithms/
+// bottum_up_array_penalty_plus_pseudo_CV.py handle_pattern :26-78 and
+// bottum_up_array_w_numba.py handle_pattern :31-64); the layout is ours:
+//
+//   cell index  n = l + B * h        l = low part (positions 0..t-1), h = high part
+//   S[h][lane][Bpad]  f32  train score of cell (h,l) for one lane (lane = one penalty of
+//                          one (alpha, fold) group)
+//   C[h][lane][Bpad]  u8   argmin code: (position << 3) | pair, or KP_SINGLE
+//   K[h][kl][nf][2]   CT   fold counts (M, U) of the block's k-mer-low cells kl
+//
+// Tie rule: the reference scans positions 0..k-1, pairs in table order, with a strict
+// "<" starting from +inf, then the single-pattern term with a strict "<" in float64.
+// The scan is split here into (low positions, in LDS) and (high positions, gathered);
+// low positions come first in scan order, so the low winner beats the high winner on
+// equal value.  NaN candidates never win, exactly as with the sequential scan.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define KP_MAXK 16          // pattern length limit (15^16 cells is far beyond any HBM)
+#define KP_MAXT 8           // low positions per block
+#define KP_GROUP_LANES 8    // penalties per (alpha, fold) group
+#define KP_SINGLE 0xFFu     // argmin code: keep the cell as one pattern
+#define KP_NONE 0xFEu       // argmin code: no candidate (only +inf/NaN seen)
+#define KP_MAX_HPAIRS 128   // high split pairs of one block (<= (k-t) * 7)
+#define KP_MAXDEPTH (3 * KP_MAXK + 2)
+
+// per position: for every digit its level, number of split pairs and the digit pairs
+struct kp_postab {
+    uint8_t lev[16];
+    uint8_t np[16];
+    uint8_t pa[16][8];
+    uint8_t pb[16][8];
+};
+
+// one (alpha, fold) group of lanes; fold < 0 = fit mode (train counts = all data)
+struct kp_group_dev {
+    int32_t fold;
+    int32_t lane0;
+    int32_t nl;
+    int32_t pad_;
+    double alpha;
+    double beta;
+    double pen[KP_GROUP_LANES];
+};
+
+// lattice geometry, passed by value to every kernel
+struct kp_geom {
+    int k, t, kh;          // positions, low positions, high positions
+    int nf;                // folds held in K
+    uint32_t B, Bpad;      // cells per block, padded row length (multiple of 16)
+    uint32_t n_kl;         // k-mer-low cells per block
+    uint32_t Ltot;         // lanes held in S / C
+    uint64_t nblocks;      // number of blocks = npat / B
+    uint32_t r[KP_MAXK];   // radix of every position
+    uint32_t n[KP_MAXK];   // nucleotides of every position's general code
+    uint64_t cgl[KP_MAXK]; // global place value of every position (cell index units)
+    uint64_t hcg[KP_MAXK]; // place value of high position i (block index units)
+    uint64_t khw[KP_MAXK]; // k-mer index weight of high position i
+};
+
+struct kp_cnt {
+    uint64_t mtr, utr, mte, ute;  // train / test counts of one cell for one fold
+};
+
+struct kp_hpair {
+    uint64_t h1, h2;  // child blocks
+    uint32_t code;    // argmin code of this split
+    uint32_t pad_;
+};
+
+// ---------------------------------------------------------------------------
+// scoring arithmetic (float64, order of operations as in the reference)
+// ---------------------------------------------------------------------------
+
+// scipy.special.xlogy / xlog1py: 0 when x == 0 and y is not NaN
+__host__ __device__ inline double kp_xlogy(double x, double y) {
+    return (x == 0.0 && y == y) ? 0.0 : x * log(y);  // y == y: not NaN
+}
+__host__ __device__ inline double kp_xlog1py(double x, double y) {
+    return (x == 0.0 && y == y) ? 0.0 : x * log1p(y);
+}
+
+// p = (M_tr + a) / (M_tr + U_tr + a + beta), summed left to right (CV :60, Fit :56)
+__host__ __device__ inline double kp_rate(const kp_cnt &c, double a, double b) {
+    return ((double)c.mtr + a) / (((double)(c.mtr + c.utr) + a) + b);
+}
+
+// k-mer cell: -2*(xlogy(M,p) + xlog1py(U,-p)) + c  (CV score_test_folds :15-20, Fit score :26-29)
+__host__ __device__ inline float kp_kmer_train(const kp_cnt &c, double a, double b, double pen) {
+    double p = kp_rate(c, a, b);
+    return (float)(-2.0 * (kp_xlogy((double)c.mtr, p) + kp_xlog1py((double)c.utr, -p)) + pen);
+}
+__host__ __device__ inline float kp_kmer_test(const kp_cnt &c, double a, double b) {
+    double p = kp_rate(c, a, b);
+    return (float)(-2.0 * (kp_xlogy((double)c.mte, p) + kp_xlog1py((double)c.ute, -p)));
+}
+
+// level >= 1 single-pattern term: c + (-2 M) log p + (-2 U) log(1-p)  (CV :63-70, Fit :56-61)
+__host__ __device__ inline double kp_single_train(const kp_cnt &c, double logp, double log1mp, double pen) {
+    double s = pen;
+    if (c.mtr > 0) s += (-2.0 * (double)c.mtr) * logp;
+    if (c.utr > 0) s += (-2.0 * (double)c.utr) * log1mp;
+    return s;
+}
+// matching test -2LL (CV :73-78)
+__host__ __device__ inline float kp_single_test(const kp_cnt &c, double logp, double log1mp) {
+    double s = 0.0;
+    if (c.mte > 0) s += (-2.0 * (double)c.mte) * logp;
+    if (c.ute > 0) s += (-2.0 * (double)c.ute) * log1mp;
+    return (float)s;
+}
+
+// ---------------------------------------------------------------------------
+// counts
+// ---------------------------------------------------------------------------
+
+// counts of one k-mer-low cell of block h for group fold f (f < 0: fit mode)
+template <typename CT>
+__host__ __device__ inline kp_cnt kp_kl_counts(const kp_geom &g, const CT *K, uint64_t h, uint32_t kl, int fold) {
+    const CT *row = K + ((h * g.n_kl + kl) * (uint64_t)g.nf) * 2;
+    uint64_t sm = 0, su = 0;
+    for (int f = 0; f < g.nf; ++f) {
+        sm += (uint64_t)row[2 * f];
+        su += (uint64_t)row[2 * f + 1];
+    }
+    kp_cnt c;
+    if (fold < 0) {
+        c.mtr = sm; c.utr = su; c.mte = 0; c.ute = 0;
+    } else {
+        c.mte = (uint64_t)row[2 * fold];
+        c.ute = (uint64_t)row[2 * fold + 1];
+        c.mtr = sm - c.mte;  // get_train (CV :22-24, :56-59): fold total minus the fold
+        c.utr = su - c.ute;
+    }
+    return c;
+}
+
+// ---------------------------------------------------------------------------
+// digits
+// ---------------------------------------------------------------------------
+
+__host__ __device__ inline uint32_t kp_low_digit(uint32_t lowinfo, int i) { return (lowinfo >> (4 * i)) & 15u; }
+
+// digit of high position i (0-based among high positions) of block h
+__host__ __device__ inline uint32_t kp_high_digit(const kp_geom &g, uint64_t h, int i) {
+    return (uint32_t)((h / g.hcg[i]) % g.r[g.t + i]);
+}
+
+// ordered list of the split pairs at high positions of block h (scan order)
+__host__ __device__ inline int kp_high_pairs(const kp_geom &g, const kp_postab *tabs, uint64_t h, kp_hpair *out) {
+    int np = 0;
+    for (int i = 0; i < g.kh; ++i) {
+        const kp_postab &T = tabs[g.t + i];
+        uint32_t d = kp_high_digit(g, h, i);
+        for (int j = 0; j < T.np[d]; ++j) {
+            out[np].h1 = h + ((uint64_t)T.pa[d][j] - d) * g.hcg[i];  // a < d, unsigned wrap is exact
+            out[np].h2 = h + ((uint64_t)T.pb[d][j] - d) * g.hcg[i];
+            out[np].code = (uint32_t)(((g.t + i) << 3) | j);
+            ++np;
+        }
+    }
+    return np;
+}
+
+__host__ __device__ inline int kp_high_pair_count(const kp_geom &g, const kp_postab *tabs, uint64_t h) {
+    int np = 0;
+    for (int i = 0; i < g.kh; ++i) np += tabs[g.t + i].np[kp_high_digit(g, h, i)];
+    return np;
+}
+
+__host__ __device__ inline int kp_high_level(const kp_geom &g, const kp_postab *tabs, uint64_t h) {
+    int s = 0;
+    for (int i = 0; i < g.kh; ++i) s += tabs[g.t + i].lev[kp_high_digit(g, h, i)];
+    return s;
+}
+
+// is cell (h, l) a k-mer (every digit a nucleotide)?
+__host__ __device__ inline bool kp_is_kmer(const kp_geom &g, uint64_t h, uint32_t lowinfo) {
+    for (int i = 0; i < g.t; ++i)
+        if (kp_low_digit(lowinfo, i) >= g.n[i]) return false;
+    for (int i = 0; i < g.kh; ++i)
+        if (kp_high_digit(g, h, i) >= g.n[g.t + i]) return false;
+    return true;
+}
+
+__host__ __device__ inline uint64_t kp_lane_row(const kp_geom &g, uint64_t h, uint32_t lane) {
+    return (h * g.Ltot + lane) * (uint64_t)g.Bpad;
+}
+
+// ---------------------------------------------------------------------------
+// one DP cell of one lane, inside an LDS block
+//   st / ch : this lane's block row (train values / argmin codes), children final,
+//             own slot holding the best high-position candidate from the gather phase
+// ---------------------------------------------------------------------------
+struct kp_single_ctx {
+    bool kmer;      // level-0 cell: reference uses the xlogy formula and no splits
+    double logp, log1mp;
+    kp_cnt c;
+};
+
+__host__ __device__ inline void kp_dp_cell(const kp_geom &g, const kp_postab *lowtabs, uint32_t l, uint32_t lowinfo,
+                                           float *st, uint8_t *ch, const kp_single_ctx &sc, double alpha,
+                                           double beta, double pen) {
+    float best = st[l];
+    uint32_t code = ch[l];
+    if (sc.kmer) {
+        // level 0 (CV :145-151 / Fit :106-114): the score is the k-mer's own term
+        st[l] = kp_kmer_train(sc.c, alpha, beta, pen);
+        ch[l] = (uint8_t)KP_SINGLE;
+        return;
+    }
+    // low positions first in scan order
+    float lbest = __builtin_huge_valf();
+    uint32_t lcode = KP_NONE;
+    for (int i = 0; i < g.t; ++i) {
+        uint32_t d = kp_low_digit(lowinfo, i);
+        const kp_postab &T = lowtabs[i];
+        uint32_t cg = (uint32_t)g.cgl[i];
+        for (int j = 0; j < T.np[d]; ++j) {
+            uint32_t l1 = l - (d - T.pa[d][j]) * cg;
+            uint32_t l2 = l - (d - T.pb[d][j]) * cg;
+            float v = st[l1] + st[l2];
+            if (v < lbest) {
+                lbest = v;
+                lcode = (uint32_t)((i << 3) | j);
+            }
+        }
+    }
+    // sequential-scan equivalence: a low candidate wins unless a high one is strictly lower
+    if (lcode != KP_NONE && !(best < lbest)) {
+        best = lbest;
+        code = lcode;
+    }
+    double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen);
+    if (s < (double)best) {
+        best = (float)s;
+        code = KP_SINGLE;
+    }
+    st[l] = best;
+    ch[l] = (uint8_t)code;
+}
+
+// ---------------------------------------------------------------------------
+// backtrack of one lane: DFS over the argmin tree from the root.
+// Returns the test -2LL of the root (CV :159-163) computed with the reference's f32
+// sums test[c1] + test[c2]; optionally lists leaves in reference order (Fit :17-24).
+// ---------------------------------------------------------------------------
+template <typename CT>
+__host__ __device__ inline float kp_leaf_test(const kp_geom &g, const kp_postab *tabs, const uint32_t *lowinfo_tab,
+                                              const uint32_t *klofs, const uint16_t *kllist, const CT *K,
+                                              uint64_t x, int fold, double alpha, double beta) {
+    uint64_t h = x / g.B;
+    uint32_t l = (uint32_t)(x % g.B);
+    kp_cnt c = {0, 0, 0, 0};
+    for (uint32_t q = klofs[l]; q < klofs[l + 1]; ++q) {
+        kp_cnt e = kp_kl_counts<CT>(g, K, h, kllist[q], fold);
+        c.mtr += e.mtr; c.utr += e.utr; c.mte += e.mte; c.ute += e.ute;
+    }
+    if (fold < 0) return 0.0f;
+    if (kp_is_kmer(g, h, lowinfo_tab[l])) return kp_kmer_test(c, alpha, beta);
+    double p = kp_rate(c, alpha, beta);
+    return kp_single_test(c, log(p), log(1.0 - p));
+}
+
+struct kp_frame {
+    uint64_t x, x2;
+    float v1;
+    uint32_t st;
+};
+
+template <typename CT>
+__host__ __device__ inline float kp_backtrack_lane(const kp_geom &g, const kp_postab *tabs, const uint32_t *lowinfo_tab,
+                                                   const uint32_t *klofs, const uint16_t *kllist, const CT *K,
+                                                   const uint8_t *C, uint32_t lane, int fold, double alpha,
+                                                   double beta, uint64_t *leaves, uint64_t cap,
+                                                   uint64_t *nleaves, uint32_t *bad) {
+    kp_frame stk[KP_MAXDEPTH];
+    int sp = 1;
+    stk[0].x = g.nblocks * g.B - 1;  // the general pattern is the last cell
+    stk[0].st = 0;
+    float ret = 0.0f;
+    uint64_t nl = 0;
+    uint32_t err = 0;
+    while (sp > 0) {
+        kp_frame &f = stk[sp - 1];
+        if (f.st == 0) {
+            uint64_t h = f.x / g.B;
+            uint32_t l = (uint32_t)(f.x % g.B);
+            uint32_t code = C[kp_lane_row(g, h, lane) + l];
+            if (code == KP_SINGLE || code == KP_NONE) {
+                if (code == KP_NONE) err = 1;
+                ret = kp_leaf_test<CT>(g, tabs, lowinfo_tab, klofs, kllist, K, f.x, fold, alpha, beta);
+                if (leaves && nl < cap) leaves[nl] = f.x;
+                ++nl;
+                --sp;
+            } else {
+                int i = (int)(code >> 3), j = (int)(code & 7u);
+                uint32_t d = (uint32_t)((f.x / g.cgl[i]) % g.r[i]);
+                const kp_postab &T = tabs[i];
+                uint64_t x1 = f.x - (uint64_t)(d - T.pa[d][j]) * g.cgl[i];
+                f.x2 = f.x - (uint64_t)(d - T.pb[d][j]) * g.cgl[i];
+                f.st = 1;
+                if (sp >= KP_MAXDEPTH) { err = 2; break; }
+                stk[sp].x = x1;
+                stk[sp].st = 0;
+                ++sp;
+                continue;
+            }
+        } else if (f.st == 1) {
+            f.v1 = ret;
+            f.st = 2;
+            if (sp >= KP_MAXDEPTH) { err = 2; break; }
+            stk[sp].x = f.x2;
+            stk[sp].st = 0;
+            ++sp;
+            continue;
+        } else {
+            ret = f.v1 + ret;  // f32 + f32, test[c1] + test[c2] (CV :47)
+            --sp;
+        }
+    }
+    *nleaves = nl;
+    *bad = err;
+    return ret;
+}

@@ -1,0 +1,186 @@
+// kp_plan.h -- host-side construction of the blocked lattice plan.
+//
+// Input: a general IUPAC pattern (e.g. "NNNNMNNNN").  Output: every table the kernels
+// need (kp_core.h).  The IUPAC data restates src/kmerpapa/pattern_utils.py:5-100 of the
+// reference (code, perm_code, complements); the digit of a sub-code is its index in
+// perm_code[g] and the cell index is mixed radix with position 0 least significant
+// (PatternEnumeration, pattern_utils.py:247-266).
+#pragma once
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "kp_core.h"
+
+namespace kp {
+
+static const char *const kIupac = "ACGTRYSWKMBDHVN";
+static const char *const kNuc[15] = {"A", "C", "G", "T", "AG", "CT", "GC", "AT", "GT", "AC",
+                                     "CGT", "AGT", "ACT", "ACG", "ACGT"};
+static const char *const kPerm[15] = {"A", "C", "G", "T", "AGR", "CTY", "GCS", "ATW", "GTK", "ACM",
+                                      "CGTSYKB", "AGTRWKD", "ACTMWYH", "ACGMRSV", "ACGTRYSWKMBDHVN"};
+// split pairs, two letters per pair, in scan order
+static const char *const kSplit[15] = {"", "", "", "", "AG", "CT", "GC", "AT", "GT", "AC",
+                                       "CKGYTS", "AKGWTR", "AYCWTM", "ASCRGM", "SWKMRYABCDGHTV"};
+
+inline int iupac_index(char c) {
+    if (!c) return -1;
+    const char *p = strchr(kIupac, c);
+    return p ? (int)(p - kIupac) : -1;
+}
+
+struct host_plan {
+    std::string gp;
+    kp_geom g;
+    uint64_t npat = 0;
+    int maxlev = 0, hmax = 0, lmax = 0;
+    uint64_t n_kmers = 0;
+    std::vector<kp_postab> tabs;       // [k]
+    std::vector<uint32_t> lowinfo;     // [B] packed low digits
+    std::vector<uint16_t> lorder;      // [B] low cells sorted by low level
+    std::vector<int32_t> loff;         // [lmax + 2]
+    std::vector<uint32_t> klofs;       // [B + 1]
+    std::vector<uint16_t> kllist;      // k-mer-low cells matching each low cell
+    std::vector<uint32_t> hlist;       // [nblocks] blocks sorted by high level
+    std::vector<uint64_t> hoff;        // [hmax + 2]
+    uint32_t kh_nuc_weight = 0;
+    // algorithmic accounting: split pairs summed over all cells
+    double pairs_total = 0.0, pairs_low = 0.0, pairs_high = 0.0;
+};
+
+// Build the plan.  max_block bounds the LDS block (cells); returns "" or an error text.
+inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan &P) {
+    P = host_plan();
+    P.gp = gen_pat ? gen_pat : "";
+    int k = (int)P.gp.size();
+    if (k <= 0 || k > KP_MAXK) return "general pattern length must be 1.." + std::to_string(KP_MAXK);
+    kp_geom &g = P.g;
+    memset(&g, 0, sizeof(g));
+    g.k = k;
+    P.tabs.resize(k);
+    memset(P.tabs.data(), 0, sizeof(kp_postab) * k);
+    uint64_t acc = 1, kacc = 1;
+    std::vector<uint64_t> kw(k);
+    for (int i = 0; i < k; ++i) {
+        int gi = iupac_index(P.gp[i]);
+        if (gi < 0) return std::string("not an IUPAC code: ") + P.gp[i];
+        const char *perm = kPerm[gi];
+        int r = (int)strlen(perm);
+        g.r[i] = (uint32_t)r;
+        g.n[i] = (uint32_t)strlen(kNuc[gi]);
+        g.cgl[i] = acc;
+        kw[i] = kacc;
+        if (acc > (~0ULL) / (uint64_t)r) return "lattice too large";
+        acc *= (uint64_t)r;
+        kacc *= g.n[i];
+        P.maxlev += (int)g.n[i] - 1;
+        for (int d = 0; d < r; ++d) {
+            int x = iupac_index(perm[d]);
+            P.tabs[i].lev[d] = (uint8_t)(strlen(kNuc[x]) - 1);
+            const char *sp = kSplit[x];
+            int np = (int)strlen(sp) / 2;
+            P.tabs[i].np[d] = (uint8_t)np;
+            for (int j = 0; j < np; ++j) {
+                P.tabs[i].pa[d][j] = (uint8_t)(strchr(perm, sp[2 * j]) - perm);
+                P.tabs[i].pb[d][j] = (uint8_t)(strchr(perm, sp[2 * j + 1]) - perm);
+            }
+        }
+    }
+    P.npat = acc;
+    P.n_kmers = kacc;
+    // low positions: as many as fit the block budget
+    int t = 0;
+    while (t < k && t < KP_MAXT && g.cgl[t] * g.r[t] <= (uint64_t)max_block) ++t;
+    if (t == 0) t = 1;  // a single position always fits (radix <= 15)
+    g.t = t;
+    g.kh = k - t;
+    g.B = (uint32_t)(t < k ? g.cgl[t] : acc);
+    g.Bpad = (g.B + 15u) & ~15u;
+    g.nblocks = acc / g.B;
+    uint32_t nkl = 1;
+    for (int i = 0; i < t; ++i) nkl *= g.n[i];
+    g.n_kl = nkl;
+    for (int i = 0; i < g.kh; ++i) {
+        g.hcg[i] = g.cgl[t + i] / g.B;
+        g.khw[i] = kw[t + i];
+    }
+    // low cells: digits, levels, order, matching k-mer-low cells
+    uint32_t B = g.B;
+    P.lowinfo.resize(B);
+    std::vector<int> llev(B);
+    int lmax = 0;
+    for (int i = 0; i < t; ++i) lmax += (int)g.n[i] - 1;
+    P.lmax = lmax;
+    P.loff.assign(lmax + 2, 0);
+    for (uint32_t l = 0; l < B; ++l) {
+        uint32_t q = l, info = 0;
+        int s = 0;
+        for (int i = 0; i < t; ++i) {
+            uint32_t d = q % g.r[i];
+            q /= g.r[i];
+            info |= d << (4 * i);
+            s += P.tabs[i].lev[d];
+        }
+        P.lowinfo[l] = info;
+        llev[l] = s;
+        P.loff[s + 1]++;
+    }
+    for (int s = 0; s <= lmax; ++s) P.loff[s + 1] += P.loff[s];
+    P.lorder.resize(B);
+    {
+        std::vector<int32_t> fill(P.loff.begin(), P.loff.end() - 1);
+        for (uint32_t l = 0; l < B; ++l) P.lorder[fill[llev[l]]++] = (uint16_t)l;
+    }
+    // nucleotide index sets of every (position, digit): nucleotide c of code x has
+    // k-mer digit = index of c in code[g] = perm digit of c (nucleotides come first)
+    P.klofs.assign(B + 1, 0);
+    for (uint32_t l = 0; l < B; ++l) {
+        // enumerate the product of nucleotide sets of the low digits
+        std::vector<uint32_t> cur(1, 0);
+        uint32_t w = 1;
+        for (int i = 0; i < t; ++i) {
+            uint32_t d = kp_low_digit(P.lowinfo[l], i);
+            int gi = iupac_index(P.gp[i]);
+            const char *perm = kPerm[gi];
+            const char *nucs = kNuc[iupac_index(perm[d])];
+            std::vector<uint32_t> nxt;
+            for (uint32_t base : cur)
+                for (const char *c = nucs; *c; ++c) nxt.push_back(base + (uint32_t)(strchr(perm, *c) - perm) * w);
+            cur.swap(nxt);
+            w *= g.n[i];
+        }
+        for (uint32_t v : cur) P.kllist.push_back((uint16_t)v);
+        P.klofs[l + 1] = (uint32_t)P.kllist.size();
+    }
+    // blocks by high level
+    int hmax = 0;
+    for (int i = t; i < k; ++i) hmax += (int)g.n[i] - 1;
+    P.hmax = hmax;
+    P.hoff.assign(hmax + 2, 0);
+    if (g.nblocks > 0xFFFFFFFFull) return "too many blocks for 32-bit block ids";
+    std::vector<uint8_t> hl(g.nblocks);
+    for (uint64_t h = 0; h < g.nblocks; ++h) {
+        int s = kp_high_level(g, P.tabs.data(), h);
+        hl[h] = (uint8_t)s;
+        P.hoff[s + 1]++;
+    }
+    for (int s = 0; s <= hmax; ++s) P.hoff[s + 1] += P.hoff[s];
+    P.hlist.resize(g.nblocks);
+    {
+        std::vector<uint64_t> fill(P.hoff.begin(), P.hoff.end() - 1);
+        for (uint64_t h = 0; h < g.nblocks; ++h) P.hlist[fill[hl[h]]++] = (uint32_t)h;
+    }
+    // split pairs per position: sum over digits of np, times the other radices
+    for (int i = 0; i < k; ++i) {
+        double sum = 0;
+        for (uint32_t d = 0; d < g.r[i]; ++d) sum += P.tabs[i].np[d];
+        double cnt = sum * (double)(P.npat / g.r[i]);
+        P.pairs_total += cnt;
+        if (i < t) P.pairs_low += cnt; else P.pairs_high += cnt;
+    }
+    return "";
+}
+
+}  // namespace kp

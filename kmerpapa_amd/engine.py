@@ -1,0 +1,377 @@
+"""ctypes binding of ``libkmerpapa_hip.so`` (C-ABI in include/kmerpapa_hip.h).
+
+This is the only door from the Python host layer into the GPU.  There is no CPU
+fallback: if the HIP library is missing or no GPU is visible, :func:`load` / :class:`Device`
+raise, loudly.
+
+Host-side responsibilities kept here:
+  * k-mer ordering: count tables go to the device in KmerEnumeration order (position 0
+    fastest, nucleotide digit = index in ``code[g]``), see ``kmer_order``;
+  * pass planning: lane groups are packed into passes that fit device memory
+    (5 bytes per cell per lane: f32 train score + u8 argmin code);
+  * sharding: groups are spread over the visible GPUs, one host thread per GPU
+    (ctypes releases the GIL during every call), no collective needed.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+from .pattern_utils import code_no
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkmerpapa_hip.so")
+MAX_GROUP_LANES = 8
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+class KPError(RuntimeError):
+    """Error reported by the C-ABI (carries the KP_E_* code)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"kmerpapa_hip error {code}: {msg}")
+        self.code = code
+
+
+class KPGroup(ctypes.Structure):
+    _fields_ = [("fold", ctypes.c_int32), ("n_lanes", ctypes.c_int32), ("alpha", ctypes.c_double),
+                ("beta", ctypes.c_double), ("penalty", ctypes.c_double * MAX_GROUP_LANES)]
+
+
+class KPPlanInfo(ctypes.Structure):
+    _fields_ = [("npat", ctypes.c_uint64), ("nblocks", ctypes.c_uint64), ("n_kmers", ctypes.c_uint64),
+                ("block", ctypes.c_uint32), ("block_pad", ctypes.c_uint32), ("k", ctypes.c_int32),
+                ("low_positions", ctypes.c_int32), ("max_level", ctypes.c_int32),
+                ("high_levels", ctypes.c_int32), ("pairs_total", ctypes.c_double),
+                ("pairs_high", ctypes.c_double), ("bytes_per_lane", ctypes.c_uint64)]
+
+
+class KPPassStats(ctypes.Structure):
+    _fields_ = [("dp_ms", ctypes.c_double), ("backtrack_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("units", ctypes.c_uint64), ("dp_launches", ctypes.c_uint64), ("alg_bytes", ctypes.c_double),
+                ("gather_bytes", ctypes.c_double)]
+
+
+EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
+           "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_pass", "kp_last_pass_stats",
+           "kp_fit_leaves", "kp_dump_lane"]
+
+
+def load():
+    """Load libkmerpapa_hip.so (built in-tree by __graft_entry__.build())."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                              "g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        vp = ctypes.c_void_p
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.kp_last_error.restype = ctypes.c_char_p
+        L.kp_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.kp_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        L.kp_destroy.argtypes = [vp]
+        L.kp_destroy.restype = None
+        L.kp_device_mem.argtypes = [vp, u64p, u64p]
+        L.kp_plan_create.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(vp)]
+        L.kp_plan_destroy.argtypes = [vp]
+        L.kp_plan_destroy.restype = None
+        L.kp_plan_get_info.argtypes = [vp, ctypes.POINTER(KPPlanInfo)]
+        L.kp_set_counts.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.kp_pass.argtypes = [vp, ctypes.POINTER(KPGroup), ctypes.c_int, vp, vp, vp]
+        L.kp_last_pass_stats.argtypes = [vp, ctypes.POINTER(KPPassStats)]
+        L.kp_fit_leaves.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u64p]
+        L.kp_dump_lane.argtypes = [vp, ctypes.c_uint32, vp, vp]
+        for name in EXPORTS:
+            if name not in ("kp_destroy", "kp_plan_destroy", "kp_last_error"):
+                getattr(L, name).restype = ctypes.c_int
+        _lib = L
+        return L
+
+
+def _check(rc):
+    if rc != 0:
+        raise KPError(rc, load().kp_last_error().decode(errors="replace"))
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _check(load().kp_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def visible_devices():
+    """GPUs the DP may use: $KMERPAPA_DEVICES (comma list) or every visible device."""
+    env = os.environ.get("KMERPAPA_DEVICES")
+    if env:
+        return [int(x) for x in env.split(",") if x.strip()]
+    return list(range(device_count()))
+
+
+class Device:
+    """One HIP device context (stream + events) of the library."""
+
+    def __init__(self, device=0):
+        L = load()
+        self.device = device
+        self._h = ctypes.c_void_p()
+        _check(L.kp_create(int(device), ctypes.byref(self._h)))
+
+    def mem(self):
+        fr, tot = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(load().kp_device_mem(self._h, ctypes.byref(fr), ctypes.byref(tot)))
+        return fr.value, tot.value
+
+    def close(self):
+        if self._h:
+            load().kp_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Plan:
+    """The lattice of one general pattern on one device, with its resident buffers."""
+
+    def __init__(self, device, gen_pat, max_block=0):
+        self.device = device
+        self.gen_pat = gen_pat
+        self._h = ctypes.c_void_p()
+        _check(load().kp_plan_create(device._h, gen_pat.encode(), ctypes.c_uint32(max_block), ctypes.byref(self._h)))
+        info = KPPlanInfo()
+        _check(load().kp_plan_get_info(self._h, ctypes.byref(info)))
+        self.info = {name: getattr(info, name) for name, _ in KPPlanInfo._fields_}
+        self.nf = None
+        self.itype = None
+        self.last_lanes = 0
+
+    def set_counts(self, M, U):
+        """Fold counts ``[n_kmers, nf]`` (uint32/uint64) in KmerEnumeration order."""
+        M = np.ascontiguousarray(M)
+        if M.dtype not in (np.uint32, np.uint64):
+            raise TypeError("counts must be uint32 or uint64")
+        U = np.ascontiguousarray(U, dtype=M.dtype)
+        if M.ndim == 1:
+            M = M.reshape(-1, 1)
+            U = U.reshape(-1, 1)
+        _check(load().kp_set_counts(self._h, _ptr(M), _ptr(U), ctypes.c_uint64(M.shape[0]), int(M.shape[1]),
+                                    int(M.dtype.itemsize)))
+        self.nf = M.shape[1]
+        self.itype = M.dtype
+
+    def run(self, groups):
+        """One DP sweep.  ``groups``: list of ``(fold, alpha, beta, penalties)``.
+
+        Returns ``(root_train f32[L], root_test f32[L], n_leaves u64[L])`` with lanes
+        numbered group-major.
+        """
+        arr = (KPGroup * len(groups))()
+        nl = 0
+        for i, (fold, alpha, beta, pens) in enumerate(groups):
+            pens = list(pens)
+            if not 1 <= len(pens) <= MAX_GROUP_LANES:
+                raise ValueError("a group holds 1..8 penalties")
+            arr[i].fold = int(fold)
+            arr[i].n_lanes = len(pens)
+            arr[i].alpha = float(alpha)
+            arr[i].beta = float(beta)
+            for j, c in enumerate(pens):
+                arr[i].penalty[j] = float(c)
+            nl += len(pens)
+        rt = np.zeros(nl, np.float32)
+        re = np.zeros(nl, np.float32)
+        nlv = np.zeros(nl, np.uint64)
+        _check(load().kp_pass(self._h, arr, len(groups), _ptr(rt), _ptr(re), _ptr(nlv)))
+        self.last_lanes = nl
+        return rt, re, nlv
+
+    def stats(self):
+        s = KPPassStats()
+        _check(load().kp_last_pass_stats(self._h, ctypes.byref(s)))
+        return {name: getattr(s, name) for name, _ in KPPassStats._fields_}
+
+    def leaves(self, lane):
+        """Cell indices of the optimal partition of ``lane``, in backtrack order."""
+        n = ctypes.c_uint64()
+        _check(load().kp_fit_leaves(self._h, int(lane), None, ctypes.c_uint64(0), ctypes.byref(n)))
+        out = np.zeros(max(1, n.value), np.uint64)
+        _check(load().kp_fit_leaves(self._h, int(lane), _ptr(out), ctypes.c_uint64(out.size), ctypes.byref(n)))
+        return out[:n.value]
+
+    def dump_lane(self, lane):
+        score = np.zeros(self.info["npat"], np.float32)
+        code = np.zeros(self.info["npat"], np.uint8)
+        _check(load().kp_dump_lane(self._h, int(lane), _ptr(score), _ptr(code)))
+        return score, code
+
+    def lanes_that_fit(self, reserve=2 << 30):
+        fr, _ = self.device.mem()
+        per = self.info["bytes_per_lane"]
+        # buffers of the current pass are reused: count them as available
+        held = self.last_lanes * per
+        return max(0, int((fr + held - reserve) // per))
+
+    def close(self):
+        if self._h:
+            load().kp_plan_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ----------------------------------------------------------------------------
+# host helpers
+# ----------------------------------------------------------------------------
+
+def kmer_order(gen_pat, contexts):
+    """KmerEnumeration index of every k-mer string in ``contexts`` (vectorised)."""
+    k = len(gen_pat)
+    if not contexts:
+        return np.zeros(0, np.int64)
+    raw = np.frombuffer("".join(contexts).encode("ascii"), dtype=np.uint8).reshape(len(contexts), k)
+    idx = np.zeros(len(contexts), np.int64)
+    w = 1
+    for i, g in enumerate(gen_pat):
+        lut = np.full(256, -1, np.int64)
+        for nuc, d in code_no[g].items():
+            lut[ord(nuc)] = d
+        dig = lut[raw[:, i]]
+        if (dig < 0).any():
+            bad = contexts[int(np.argmax(dig < 0))]
+            raise ValueError(f"k-mer {bad} does not match general pattern {gen_pat}")
+        idx += dig * w
+        w *= len(code_no[g])
+    return idx
+
+
+def counts_in_kmer_order(gen_pat, contexts, M, U, n_kmers, itype):
+    """Scatter per-context rows ``[n, nf]`` into dense KmerEnumeration order (missing k-mers = 0)."""
+    M = np.asarray(M)
+    nf = 1 if M.ndim == 1 else M.shape[1]
+    outM = np.zeros((n_kmers, nf), dtype=itype)
+    outU = np.zeros((n_kmers, nf), dtype=itype)
+    idx = kmer_order(gen_pat, list(contexts))
+    outM[idx] = np.asarray(M, dtype=itype).reshape(len(idx), nf)
+    outU[idx] = np.asarray(U, dtype=itype).reshape(len(idx), nf)
+    return outM, outU
+
+
+def pack_passes(groups, max_lanes):
+    """Split a group list into passes of at most ``max_lanes`` lanes (order kept)."""
+    if max_lanes < 1:
+        raise KPError(-2, "the lattice does not fit device memory even for one lane")
+    passes, cur, n = [], [], 0
+    for grp in groups:
+        lanes = len(grp[3])
+        if cur and n + lanes > max_lanes:
+            passes.append(cur)
+            cur, n = [], 0
+        cur.append(grp)
+        n += lanes
+    if cur:
+        passes.append(cur)
+    return passes
+
+
+_devices = {}
+_plans = {}
+_cache_lock = threading.Lock()
+
+
+def get_device(dev):
+    with _cache_lock:
+        if dev not in _devices:
+            _devices[dev] = Device(dev)
+        return _devices[dev]
+
+
+def get_plan(dev, gen_pat, max_block=0):
+    key = (dev, gen_pat, max_block)
+    with _cache_lock:
+        plan = _plans.get(key)
+    if plan is None:
+        plan = Plan(get_device(dev), gen_pat, max_block)
+        with _cache_lock:
+            # one resident lattice per device: drop other patterns' buffers first
+            for other in [k for k in _plans if k[0] == dev and k != key]:
+                _plans.pop(other).close()
+            _plans[key] = plan
+    return plan
+
+
+def release_all():
+    with _cache_lock:
+        for p in _plans.values():
+            p.close()
+        _plans.clear()
+
+
+def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
+    """Run every lane group over the lattice of ``gen_pat`` on the given GPUs.
+
+    ``M``/``U`` are ``[n_kmers, nf]`` counts in k-mer order.  Groups are dealt out in
+    contiguous chunks (one chunk per GPU), each chunk packed into memory-sized passes.
+    Returns ``(root_train, root_test, n_leaves)`` arrays over all lanes, group-major.
+    """
+    devices = list(devices) if devices is not None else visible_devices()[:1]
+    if not devices:
+        raise KPError(-3, "no GPU visible")
+    lane_counts = [len(g[3]) for g in groups]
+    total = sum(lane_counts)
+    # contiguous chunks of roughly equal lanes
+    bounds, acc, d = [0], 0, 0
+    for i, n in enumerate(lane_counts):
+        acc += n
+        if d < len(devices) - 1 and acc >= total * (d + 1) / len(devices):
+            bounds.append(i + 1)
+            d += 1
+    while len(bounds) < len(devices) + 1:
+        bounds.append(len(groups))
+    results = [None] * len(devices)
+    errors = []
+
+    def work(slot, dev, chunk):
+        try:
+            plan = get_plan(dev, gen_pat, max_block)
+            plan.set_counts(M, U)
+            outs = []
+            for pas in pack_passes(chunk, plan.lanes_that_fit()):
+                outs.append(plan.run(pas))
+            if outs:
+                results[slot] = tuple(np.concatenate([o[i] for o in outs]) for i in range(3))
+            else:
+                results[slot] = (np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(0, np.uint64))
+        except Exception as e:  # re-raised in the caller's thread
+            errors.append(e)
+
+    threads = []
+    for slot, dev in enumerate(devices):
+        chunk = groups[bounds[slot]:bounds[slot + 1]]
+        if len(devices) == 1:
+            work(slot, dev, chunk)
+        else:
+            th = threading.Thread(target=work, args=(slot, dev, chunk))
+            th.start()
+            threads.append(th)
+    for th in threads:
+        th.join()
+    if errors:
+        raise errors[0]
+    return tuple(np.concatenate([r[i] for r in results]) for i in range(3))

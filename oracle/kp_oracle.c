@@ -1,0 +1,260 @@
+/*
+ * kp_oracle.c -- CPU restatement of kmerPaPa's penalized-likelihood lattice DP.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker: tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; the product path (kmerpapa_amd/) never
+ * does.  It restates, cell by cell and in the reference's order of operations, the two
+ * numba kernels of BesenbacherLab/kmerPaPa v0.2.4:
+ *
+ *   kpo_cv  : src/kmerpapa/algorithms/bottum_up_array_penalty_plus_pseudo_CV.py
+ *             score_test_folds :15-20, get_train :22-24, handle_pattern :26-78,
+ *             driver loop :143-157
+ *   kpo_fit : src/kmerpapa/algorithms/bottum_up_array_w_numba.py
+ *             score :26-29, handle_pattern :31-64, driver :67-124
+ *
+ * Lattice tables follow src/kmerpapa/pattern_utils.py:5-100 (IUPAC code, perm_code,
+ * complements).  Parity is pinned by tests/test_oracle_golden.py against vectors the
+ * reference itself produced (tests/golden/make_golden.py).
+ *
+ * Arithmetic notes (why each line is written the way it is):
+ *  - scores are stored as float32 (ftype = np.float32, CV :89, Fit :79); split sums are
+ *    float32 + float32; the single-pattern term is float64 and compared as float64
+ *    against the float32 store (numba / numpy<2 promotion) before rounding to float32.
+ *  - counts are itype = uint32 or uint64 (CV :94-97); aggregation wraps at itype width;
+ *    fold totals are summed in uint64 (numpy sum of uint32 -> uint64).
+ *  - level 0 uses xlogy / xlog1py (scipy: 0 if x == 0 and y is not NaN) in the order
+ *    -2*(a+b)+c; levels >= 1 use log(p), log(1-p) in the order c + a + b.
+ *  Build with -ffp-contract=off (no fused multiply-add), -O2, no fast-math.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define KPO_MAXK 32
+
+typedef struct {
+    int k;
+    int radix[KPO_MAXK];
+    uint64_t cg[KPO_MAXK];
+    int lev[KPO_MAXK][16];
+    int np[KPO_MAXK][16];
+    int pa[KPO_MAXK][16][7];
+    int pb[KPO_MAXK][16][7];
+    uint64_t npat;
+    int maxlev;
+} kpo_lat;
+
+/* IUPAC data, pattern_utils.py:5-19 (code), :86-100 (perm_code), :48-57 (complements) */
+static const char *IU_CODES = "ACGTRYSWKMBDHVN";
+static const char *IU_NUC[15] = {"A", "C", "G", "T", "AG", "CT", "GC", "AT", "GT", "AC",
+                                 "CGT", "AGT", "ACT", "ACG", "ACGT"};
+static const char *IU_PERM[15] = {"A", "C", "G", "T", "AGR", "CTY", "GCS", "ATW", "GTK", "ACM",
+                                  "CGTSYKB", "AGTRWKD", "ACTMWYH", "ACGMRSV", "ACGTRYSWKMBDHVN"};
+static const char *IU_SPLIT[15] = {"", "", "", "", "AG", "CT", "GC", "AT", "GT", "AC",
+                                   "CKGYTS", "AKGWTR", "AYCWTM", "ASCRGM", "SWKMRYABCDGHTV"};
+
+static int iu_index(char c) {
+    const char *p = strchr(IU_CODES, c);
+    return (p && c) ? (int)(p - IU_CODES) : -1;
+}
+
+static int lat_build(const char *gp, kpo_lat *L) {
+    memset(L, 0, sizeof(*L));
+    L->k = (int)strlen(gp);
+    if (L->k <= 0 || L->k > KPO_MAXK) return -1;
+    uint64_t acc = 1;
+    for (int i = 0; i < L->k; ++i) {
+        int g = iu_index(gp[i]);
+        if (g < 0) return -1;
+        const char *perm = IU_PERM[g];
+        int r = (int)strlen(perm);
+        L->radix[i] = r;
+        L->cg[i] = acc;
+        acc *= (uint64_t)r;
+        L->maxlev += (int)strlen(IU_NUC[g]) - 1;
+        for (int d = 0; d < r; ++d) {
+            int x = iu_index(perm[d]);
+            L->lev[i][d] = (int)strlen(IU_NUC[x]) - 1;
+            const char *sp = IU_SPLIT[x];
+            int n = (int)strlen(sp) / 2;
+            L->np[i][d] = n;
+            for (int j = 0; j < n; ++j) {
+                L->pa[i][d][j] = (int)(strchr(perm, sp[2 * j]) - perm);
+                L->pb[i][d][j] = (int)(strchr(perm, sp[2 * j + 1]) - perm);
+            }
+        }
+    }
+    L->npat = acc;
+    return 0;
+}
+
+/* cells bucketed by level, ascending index inside a level (the reference walks a level in
+ * subpatterns_level_ord_np order; the order inside a level does not change any value
+ * because a cell only reads strictly lower levels). */
+static uint64_t *level_order(const kpo_lat *L, uint64_t *off /* [maxlev+2] */) {
+    uint64_t *out = (uint64_t *)malloc(sizeof(uint64_t) * L->npat);
+    uint8_t *lv = (uint8_t *)malloc(L->npat);
+    if (!out || !lv) { free(out); free(lv); return NULL; }
+    memset(off, 0, sizeof(uint64_t) * (L->maxlev + 2));
+    for (uint64_t n = 0; n < L->npat; ++n) {
+        uint64_t q = n;
+        int s = 0;
+        for (int i = 0; i < L->k; ++i) { s += L->lev[i][q % L->radix[i]]; q /= L->radix[i]; }
+        lv[n] = (uint8_t)s;
+        off[s + 1]++;
+    }
+    for (int s = 0; s <= L->maxlev; ++s) off[s + 1] += off[s];
+    uint64_t *fill = (uint64_t *)calloc(L->maxlev + 1, sizeof(uint64_t));
+    for (uint64_t n = 0; n < L->npat; ++n) out[off[lv[n]] + fill[lv[n]]++] = n;
+    free(fill);
+    free(lv);
+    return out;
+}
+
+static inline double xlogy_(double x, double y) { return (x == 0.0 && !isnan(y)) ? 0.0 : x * log(y); }
+static inline double xlog1py_(double x, double y) { return (x == 0.0 && !isnan(y)) ? 0.0 : x * log1p(y); }
+
+uint64_t kpo_npat(const char *gp) {
+    kpo_lat L;
+    return lat_build(gp, &L) ? 0 : L.npat;
+}
+
+/*
+ * CV pass for one (alpha, penalty) over all folds.
+ *   M, U  : [npat][nf] counts; the k-mer (level-0) rows are inputs, all other rows are
+ *           outputs (aggregated like the reference, wrapping at itype_bits).
+ *   betas : [nf]
+ *   score, test : [npat][nf] float32 outputs (train score and test -2LL of every cell).
+ */
+int kpo_cv(const char *gp, int nf, uint64_t *M, uint64_t *U, int itype_bits,
+           double alpha, const double *betas, double penalty, float *score, float *test) {
+    kpo_lat L;
+    if (lat_build(gp, &L) || nf <= 0 || nf > 64) return -1;
+    const uint64_t mask = itype_bits >= 64 ? ~0ULL : ((1ULL << itype_bits) - 1);
+    uint64_t off[KPO_MAXK * 3 + 2];
+    uint64_t *ord = level_order(&L, off);
+    if (!ord) return -2;
+    const float inf32 = (float)1e100; /* np.full(..., 1e100, float32) -> +inf (CV :143) */
+    for (uint64_t n = 0; n < L.npat * (uint64_t)nf; ++n) { score[n] = inf32; test[n] = 0.0f; }
+
+    /* level 0: score_test_folds (CV :15-20) on every k-mer row, get_train (:22-24) */
+    for (uint64_t q = off[0]; q < off[1]; ++q) {
+        uint64_t n = ord[q];
+        const uint64_t *m = M + n * nf, *u = U + n * nf;
+        uint64_t sm = 0, su = 0;
+        for (int f = 0; f < nf; ++f) { sm += m[f]; su += u[f]; }
+        for (int f = 0; f < nf; ++f) {
+            uint64_t trm = sm - m[f], tru = su - u[f];
+            double p = ((double)trm + alpha) / (((double)(trm + tru) + alpha) + betas[f]);
+            double tr = -2.0 * (xlogy_((double)trm, p) + xlog1py_((double)tru, -p)) + penalty;
+            double te = -2.0 * (xlogy_((double)m[f], p) + xlog1py_((double)u[f], -p));
+            score[n * nf + f] = (float)tr;
+            test[n * nf + f] = (float)te;
+        }
+    }
+    /* levels >= 1: handle_pattern (CV :26-78) */
+    for (uint64_t q = off[1]; q < off[L.maxlev + 1]; ++q) {
+        uint64_t n = ord[q];
+        float *rs = score + n * nf, *rt = test + n * nf;
+        int first = 1;
+        uint64_t rest = n;
+        for (int i = 0; i < L.k; ++i) {
+            int d = (int)(rest % L.radix[i]);
+            rest /= L.radix[i];
+            for (int j = 0; j < L.np[i][d]; ++j) {
+                uint64_t base = n - (uint64_t)d * L.cg[i];
+                uint64_t c1 = base + (uint64_t)L.pa[i][d][j] * L.cg[i];
+                uint64_t c2 = base + (uint64_t)L.pb[i][d][j] * L.cg[i];
+                for (int f = 0; f < nf; ++f) {
+                    float nt = score[c1 * nf + f] + score[c2 * nf + f];
+                    float ne = test[c1 * nf + f] + test[c2 * nf + f];
+                    if (nt < rs[f]) { rs[f] = nt; rt[f] = ne; }
+                }
+                if (first) {
+                    for (int f = 0; f < nf; ++f) {
+                        M[n * nf + f] = (M[c1 * nf + f] + M[c2 * nf + f]) & mask;
+                        U[n * nf + f] = (U[c1 * nf + f] + U[c2 * nf + f]) & mask;
+                    }
+                    first = 0;
+                }
+            }
+        }
+        const uint64_t *m = M + n * nf, *u = U + n * nf;
+        uint64_t sm = 0, su = 0;
+        for (int f = 0; f < nf; ++f) { sm += m[f]; su += u[f]; }
+        for (int f = 0; f < nf; ++f) {
+            uint64_t trm = sm - m[f], tru = su - u[f];
+            double p = ((double)trm + alpha) / (((double)(trm + tru) + alpha) + betas[f]);
+            double logp = log(p), log1mp = log(1.0 - p);
+            double s = penalty;
+            if (trm > 0) s += (-2.0 * (double)trm) * logp;
+            if (tru > 0) s += (-2.0 * (double)tru) * log1mp;
+            if (s < (double)rs[f]) {
+                rs[f] = (float)s;
+                double t = 0.0;
+                if (m[f] > 0) t += (-2.0 * (double)m[f]) * logp;
+                if (u[f] > 0) t += (-2.0 * (double)u[f]) * log1mp;
+                rt[f] = (float)t;
+            }
+        }
+    }
+    free(ord);
+    return 0;
+}
+
+/*
+ * Fit DP (one fold, full data) with back-pointers.
+ *   M, U      : [npat]; k-mer rows are inputs, the rest outputs.
+ *   score     : [npat] float32 output, backtrack : [npat] output (c1 of the winning split,
+ *               or the cell itself when it is kept whole), as Fit :46-49, :62-64.
+ */
+int kpo_fit(const char *gp, uint64_t *M, uint64_t *U, int itype_bits, double alpha, double beta,
+            double penalty, float *score, uint64_t *backtrack) {
+    kpo_lat L;
+    if (lat_build(gp, &L)) return -1;
+    const uint64_t mask = itype_bits >= 64 ? ~0ULL : ((1ULL << itype_bits) - 1);
+    uint64_t off[KPO_MAXK * 3 + 2];
+    uint64_t *ord = level_order(&L, off);
+    if (!ord) return -2;
+    const float inf32 = (float)1e100;
+    for (uint64_t n = 0; n < L.npat; ++n) score[n] = inf32;
+    /* level 0: score(M, U) (Fit :26-29, :106-114) */
+    for (uint64_t q = off[0]; q < off[1]; ++q) {
+        uint64_t n = ord[q];
+        double m = (double)M[n], u = (double)U[n];
+        double p = (m + alpha) / (((double)(M[n] + U[n]) + alpha) + beta);
+        score[n] = (float)(-2.0 * (xlogy_(m, p) + xlog1py_(u, -p)) + penalty);
+        backtrack[n] = n;
+    }
+    /* levels >= 1: handle_pattern (Fit :31-64) */
+    for (uint64_t q = off[1]; q < off[L.maxlev + 1]; ++q) {
+        uint64_t n = ord[q];
+        int first = 1;
+        uint64_t rest = n;
+        for (int i = 0; i < L.k; ++i) {
+            int d = (int)(rest % L.radix[i]);
+            rest /= L.radix[i];
+            for (int j = 0; j < L.np[i][d]; ++j) {
+                uint64_t base = n - (uint64_t)d * L.cg[i];
+                uint64_t c1 = base + (uint64_t)L.pa[i][d][j] * L.cg[i];
+                uint64_t c2 = base + (uint64_t)L.pb[i][d][j] * L.cg[i];
+                float ns = score[c1] + score[c2];
+                if (ns < score[n]) { score[n] = ns; backtrack[n] = c1; }
+                if (first) {
+                    M[n] = (M[c1] + M[c2]) & mask;
+                    U[n] = (U[c1] + U[c2]) & mask;
+                    first = 0;
+                }
+            }
+        }
+        uint64_t m = M[n], u = U[n];
+        double p = ((double)m + alpha) / (((double)((m + u) & mask) + alpha) + beta);
+        double s = penalty;
+        if (m > 0) s += (-2.0 * (double)m) * log(p);
+        if (u > 0) s += (-2.0 * (double)u) * log(1.0 - p);
+        if (s < (double)score[n]) { score[n] = (float)s; backtrack[n] = n; }
+    }
+    free(ord);
+    return 0;
+}

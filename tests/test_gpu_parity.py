@@ -1,0 +1,233 @@
+"""GPU parity: the HIP lattice DP (through the C-ABI) against the reference's golden
+vectors and against the CPU oracle.  Bar: bit-exact float32 scores (any NaN equals any
+NaN), identical partitions (names and order), identical CVfile text.
+"""
+import io
+import os
+import random
+
+import numpy as np
+import pytest
+
+from tests.fixtures import bits_equal, context_table, golden_json, golden_npz, write_count_files
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from kmerpapa_amd import engine
+    engine.load()
+    assert engine.device_count() >= 1, "no GPU visible to the HIP runtime"
+    return engine
+
+
+def _kmer_rows(gp, kmers, rows, dtype):
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.pattern_utils import generality
+    M, _ = engine.counts_in_kmer_order(gp, list(kmers), rows, rows, generality(gp), dtype)
+    return M
+
+
+SMALL = golden_json("small_dp.json")
+
+
+@pytest.mark.parametrize("case", ["k3", "k4", "k3zero", "k3big"])
+@pytest.mark.parametrize("max_block", [0, 16, 200])
+def test_small_lattices_full_arrays(eng, case, max_block):
+    """Every cell's f32 train score and the root test -2LL of every fold, bit for bit."""
+    c = SMALL["cases"][case]
+    A = golden_npz("small_dp.npz")
+    gp = c["gen_pat"]
+    dtype = np.uint64 if c["itype"] == "uint64" else np.uint32
+    kmers = [str(x) for x in A[f"{case}_kmers"]]
+    Mk = _kmer_rows(gp, kmers, A[f"{case}_Mf"], dtype)
+    Uk = _kmer_rows(gp, kmers, A[f"{case}_Uf"], dtype)
+    nf = Mk.shape[1]
+    plan = eng.Plan(eng.get_device(0), gp, max_block)
+    plan.set_counts(Mk, Uk)
+    for j, ps in enumerate(c["passes"]):
+        groups = [(f, ps["alpha"], ps["betas"][f], [ps["penalty"]]) for f in range(nf)]
+        rt, re, _ = plan.run(groups)
+        ref = A[f"{case}_{j}_score"]
+        for f in range(nf):
+            score, code = plan.dump_lane(f)
+            assert bits_equal(score, ref[:, f]), f"{case} pass {j} fold {f}: score array differs"
+        assert bits_equal(rt, np.array(ps["root_train"], np.float32))
+        assert bits_equal(re, np.array(ps["root_test"], np.float32))
+    plan.close()
+
+
+@pytest.mark.parametrize("case", ["k3", "k4", "k3zero", "k3big"])
+def test_small_lattice_fits(eng, case):
+    from kmerpapa_amd.algorithms import bottum_up_array_w_numba as fitm
+    c = SMALL["cases"][case]
+    ctx = {k: tuple(v) for k, v in c["contextD"].items()}
+
+    class A:
+        verbosity = 0
+    for fo in c["fits"]:
+        if "error" in fo:
+            continue  # the reference raises ZeroDivisionError for alpha=0 with an empty k-mer
+        sc, M, U, names = fitm.pattern_partition_bottom_up(c["gen_pat"], ctx, fo["alpha"], fo["beta"],
+                                                           fo["penalty"], A, c["nmut"], c["nunmut"])
+        assert float(sc) == fo["score"]
+        assert int(M) == fo["M"] and int(U) == fo["U"]
+        assert names == fo["names"]
+
+
+def test_grid5_cvfile(eng):
+    """Config 2: 5-mer 3x3 grid, 5 folds, seed 1 -> CVfile text and best (alpha, c)."""
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    g = golden_json("grid5.json")
+    ctx, gp, nm, nu = context_table(5)
+    assert gp == g["gen_pat"]
+    buf = io.StringIO()
+
+    class A:
+        nfolds = 5
+        iterations = 1
+        seed = 1
+        verbosity = 0
+        CVfile = buf
+    best = cvm.pattern_partition_bottom_up(gp, ctx, g["alphas"], A, nm, nu, g["penalties"])
+    assert buf.getvalue() == g["cvfile"]
+    assert [best[0], best[1], best[2]] == g["best"]
+
+
+def test_grid5_roots_per_fold(eng):
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    g = golden_json("grid5.json")
+    ctx, gp, nm, nu = context_table(5)
+    res = cvm.cv_roots(gp, ctx, g["alphas"], g["penalties"], 5, 1, 1, np.uint32, devices=[0])
+    for ps in g["passes"]:
+        a_i = g["alphas"].index(ps["alpha"])
+        p_i = g["penalties"].index(ps["penalty"])
+        assert bits_equal(res["test"][0, a_i, p_i], np.array(ps["root_test"], np.float32))
+        assert bits_equal(res["train"][0, a_i, p_i], np.array(ps["root_train"], np.float32))
+        assert np.array_equal(res["betas"][0, a_i], np.array(ps["betas"]))
+
+
+def test_iterations_carry_over(eng):
+    """--iterations 2 reproduces the reference's fold totals (its carry-over of the previous
+    iteration's aggregated rows, CV :134-137), roots and CVfile (5-mer, tests/golden/iter5.json)."""
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    g = golden_json("iter5.json")
+    if g is None:
+        pytest.skip("iteration golden not generated")
+    ctx, gp, nm, nu = context_table(5)
+    res = cvm.cv_roots(gp, ctx, g["alphas"], g["penalties"], g["nfolds"], g["seed"], 2, np.uint32, devices=[0])
+    for j, ps in enumerate(g["passes"]):
+        it, a_i = divmod(j, len(g["alphas"]))
+        assert np.array_equal(res["betas"][it, a_i], np.array(ps["betas"]))
+        assert bits_equal(res["test"][it, a_i, 0], np.array(ps["root_test"], np.float32))
+    buf = io.StringIO()
+
+    class A:
+        nfolds = g["nfolds"]
+        iterations = 2
+        seed = g["seed"]
+        verbosity = 0
+        CVfile = buf
+    best = cvm.pattern_partition_bottom_up(gp, ctx, g["alphas"], A, nm, nu, g["penalties"])
+    assert buf.getvalue() == g["cvfile"]
+    assert [best[0], best[1], best[2]] == g["best"]
+
+
+def test_fit5_partitions(eng):
+    from kmerpapa_amd.algorithms import bottum_up_array_w_numba as fitm
+    g = golden_json("fit5.json")
+    ctx, gp, nm, nu = context_table(5)
+
+    class A:
+        verbosity = 0
+    for fo in g["fits"]:
+        sc, M, U, names = fitm.pattern_partition_bottom_up(gp, ctx, fo["alpha"], fo["beta"], fo["penalty"], A, nm, nu)
+        assert float(sc) == fo["score"]
+        assert names == fo["names"]
+
+
+@pytest.mark.parametrize("run", ["fit", "fit_long", "grid", "super", "default_pen"])
+def test_cli5_output_text(eng, run, tmp_path, capsys):
+    """Config 1/2 through the CLI: the output table and CVfile are byte-identical."""
+    from kmerpapa_amd import cli
+    g = golden_json("cli5.json")[run]
+    pos, bg = write_count_files(5, str(tmp_path))
+    argv = []
+    for a in g["argv"]:
+        argv.append(pos if a.endswith("mutated_5mers.txt") else bg if a.endswith("background_5mers.txt") else a)
+    out = tmp_path / "o.txt"
+    cvf = tmp_path / "cv.txt"
+    rc = cli.main(argv + ["-o", str(out), "-f", str(cvf)])
+    assert rc == g["rc"]
+    assert out.read_text() == g["output"]
+    assert cvf.read_text() == g["cvfile"]
+
+
+def test_fit7_partition(eng):
+    g = golden_json("fit7.json")
+    if g is None:
+        pytest.skip("7-mer fit golden not generated")
+    from kmerpapa_amd.algorithms import bottum_up_array_w_numba as fitm
+    ctx, gp, nm, nu = context_table(7)
+
+    class A:
+        verbosity = 0
+    fo = g["fits"][0]
+    sc, M, U, names = fitm.pattern_partition_bottom_up(gp, ctx, fo["alpha"], fo["beta"], fo["penalty"], A, nm, nu)
+    assert float(sc) == fo["score"]
+    assert names == fo["names"]
+
+
+def test_cv7_roots(eng):
+    g = golden_json("cv7.json")
+    if g is None:
+        pytest.skip("7-mer CV golden not generated")
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    ctx, gp, nm, nu = context_table(7)
+    res = cvm.cv_roots(gp, ctx, g["alphas"], g["penalties"], 5, 1, 1, np.uint32, devices=[0])
+    ps = g["passes"][0]
+    assert bits_equal(res["test"][0, 0, 0], np.array(ps["root_test"], np.float32))
+    assert bits_equal(res["train"][0, 0, 0], np.array(ps["root_train"], np.float32))
+
+
+def _random_case(rng, k):
+    from kmerpapa_amd.pattern_utils import matches
+    gp = "".join(rng.choice("NNNNMRSWKYBDHVACGT") for _ in range(k))
+    ctx = {}
+    for kmer in matches(gp):
+        bg = rng.randrange(0, 5000) if rng.random() > 0.1 else 0
+        pos = rng.randrange(0, bg + 1) // rng.choice([1, 3, 30])
+        ctx[kmer] = (pos, bg - pos)
+    return gp, ctx
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_patterns_vs_oracle(eng, seed):
+    """Random general patterns (mixed IUPAC codes) and counts: GPU == oracle, all cells."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from oracle import oracle as O
+    rng = random.Random(seed)
+    gp, ctx = _random_case(rng, rng.choice([3, 4, 5]))
+    nf = rng.choice([2, 3, 5])
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(seed), np.uint32)
+    from kmerpapa_amd.pattern_utils import generality
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    alpha = rng.choice([0.1, 0.5, 2.0])
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr = tot_m.sum() - tot_m
+    utr = tot_u.sum() - tot_u
+    betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+    pens = [0.0, 2.5, 7.0]
+    plan = eng.Plan(eng.get_device(0), gp, rng.choice([0, 64]))
+    plan.set_counts(Mk, Uk)
+    rt, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
+    for pi, c in enumerate(pens):
+        ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 32)
+        for f in range(nf):
+            lane = f * len(pens) + pi
+            score, _ = plan.dump_lane(lane)
+            assert bits_equal(score, ref["score"][:, f]), (gp, c, f)
+            assert bits_equal(re[lane], ref["root_test"][f])
+    plan.close()
