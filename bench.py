@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X lattice DP on BASELINE.json's headline workload.
+
+Workload: synthetic 9-mer counts, general pattern NNNNMNNNN
+(131,072 k-mers, 7,688,671,875 lattice cells), 5x5 (pseudo-count alpha x penalty c)
+grid, 5-fold CV, fold split with seed 1 exactly as the reference does it.
+
+A step = one pass of the hot path over one batch: one (alpha, fold) group with its 5
+penalties as 5 lanes, i.e. the full DP over all 7.69e9 cells for 5 (cell, fold, alpha, c)
+units each = 3.84e10 units.  The full 5x5x5 CV is 25 such steps.  With N ranks
+(torch.distributed.run, one GPU per rank) every rank runs its own groups
+(group = (step * N + rank) mod 25): per-GPU work is fixed, "scaling": "weak", and no
+collective touches the data path; the barrier and the max-time
+reduction use gloo on the host.
+
+Timed region: K steps between two barriers; inputs (fold counts, per-block count tables)
+are resident in HBM before it starts.  Units = cells x lanes, summed over ranks.
+The roofline object prices the DP sweep kernel (kp_dp_kernel): algorithmic bytes per
+SURVEY.md §8d (16 B per split pair, 8 B per cell written, 6 s per aggregated cell, 2 s
+per k-mer, per lane) over the HIP-event duration of its launches; "traffic" is the
+PMC-measured HBM bytes per pass (profiles/, rocprofv3 FETCH_SIZE/WRITE_SIZE with the
+gfx950 x2 FETCH correction) when a matching profile summary is committed.
+The cpu_baseline leg times the CPU oracle (oracle/kp_oracle.c, a single-threaded C
+port of the reference's DP) on a bounded sample of the same counts.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+from kmerpapa_amd import engine  # noqa: E402  (loads libamdhip64 before torch does)
+from kmerpapa_amd.CV_tools import fold_tables  # noqa: E402
+from kmerpapa_amd.pattern_utils import KmerEnumeration, generality  # noqa: E402
+
+GEN_PAT = "NNNNMNNNN"
+ALPHAS = [0.5, 1.0, 2.0, 5.0, 10.0]
+PENALTIES = [3.0, 4.0, 5.0, 6.0, 7.0]
+NFOLDS = 5
+PEAK_HBM_GBS = 8000.0
+
+
+def synthetic_counts(gen_pat=GEN_PAT, seed=9):
+    """Synthetic k-mer counts, k-mers in KmerEnumeration order.
+
+    bg ~ Poisson(LogNormal(log 1.5e4, 0.8)); rate = 2.7e-5 * f[x3] * f[x5] * LogNormal(0, 0.3)
+    with f = {A: .6, C: 1, G: 1.8, T: .8} on the two bases flanking the centre;
+    positives ~ Binomial(bg, rate).  Returns (kmers, M, U).
+    """
+    rng = np.random.RandomState(seed)
+    KE = KmerEnumeration(gen_pat)
+    n = generality(gen_pat)
+    kmers = [KE.num2kmer(i) for i in range(n)]
+    bg = rng.poisson(rng.lognormal(math.log(1.5e4), 0.8, size=n))
+    f = {"A": 0.6, "C": 1.0, "G": 1.8, "T": 0.8}
+    mid = len(gen_pat) // 2
+    fl = np.array([f[k[mid - 1]] * f[k[mid + 1]] for k in kmers])
+    rate = 2.7e-5 * fl * rng.lognormal(0.0, 0.3, size=n)
+    pos = rng.binomial(bg, np.minimum(rate, 1.0))
+    return kmers, pos.astype(np.int64), (bg - pos).astype(np.int64)
+
+
+def prepare(gen_pat, seed=1):
+    """Fold split (reference RNG stream) and betas for every (alpha, fold)."""
+    kmers, M, U = synthetic_counts(gen_pat)
+    ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
+    total = int(M.sum() + U.sum())
+    itype = np.uint64 if total > np.iinfo(np.uint32).max else np.uint32
+    t0 = time.time()
+    contexts, Mf, Uf = fold_tables(ctx, NFOLDS, np.random.RandomState(seed), itype)
+    t_fold = time.time() - t0
+    Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, generality(gen_pat), itype)
+    msum = Mk.sum(axis=0, dtype=np.uint64)
+    usum = Uk.sum(axis=0, dtype=np.uint64)
+    mtr, utr = msum.sum() - msum, usum.sum() - usum
+    groups = []
+    for a in ALPHAS:
+        my = mtr / (mtr + utr)
+        betas = (a * (1.0 - my)) / my
+        for f in range(NFOLDS):
+            groups.append((f, a, float(betas[f]), list(PENALTIES)))
+    return {"Mk": Mk, "Uk": Uk, "groups": groups, "itype": itype, "t_fold_s": t_fold, "contexts": contexts,
+            "Mf": Mf, "Uf": Uf, "total": total, "gen_pat": gen_pat}
+
+
+def cpu_baseline(prep, seconds_hint=15.0):
+    """Time the single-threaded CPU oracle on a bounded sample of the same counts: the
+    sub-lattice with both outermost positions fixed to 'A' (NNNMNNN-sized, 3.4e7 cells),
+    one (alpha, c) over all 5 folds."""
+    from oracle import oracle as O
+    sub = "A" + prep["gen_pat"][1:-1] + "A"
+    keep = [i for i, c in enumerate(prep["contexts"]) if c[0] == "A" and c[-1] == "A"]
+    ctxs = [prep["contexts"][i] for i in keep]
+    Mf = prep["Mf"][keep]
+    Uf = prep["Uf"][keep]
+    g = prep["groups"][0]
+    betas = [prep["groups"][f][2] for f in range(NFOLDS)]
+    bits = 8 * np.dtype(prep["itype"]).itemsize
+    t0 = time.time()
+    O.cv_pass(sub, ctxs, Mf, Uf, g[1], betas, g[3][0], bits)
+    dt = time.time() - t0
+    units = O.npat(sub) * NFOLDS
+    return {"value": units / dt, "unit": "cells*folds*(alpha,c)/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/kp_oracle.c kpo_cv on sub-lattice {sub} of the same 9-mer counts "
+                      f"({O.npat(sub)} cells x {NFOLDS} folds, 1 (alpha,c)) in {dt:.1f} s on 1 host core"}
+
+
+def committed_traffic(gen_pat, n_lanes):
+    """HBM bytes per DP pass measured with rocprofv3 PMC counters (profiles/pmc_*.json)."""
+    best = None
+    for name in sorted(os.listdir(os.path.join(ROOT, "profiles"))) if os.path.isdir(os.path.join(ROOT, "profiles")) else []:
+        if name.startswith("pmc_") and name.endswith(".json"):
+            try:
+                d = json.load(open(os.path.join(ROOT, "profiles", name)))
+            except ValueError:
+                continue
+            if d.get("gen_pat") == gen_pat and d.get("lanes") == n_lanes:
+                best = d
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pattern", default=GEN_PAT)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--max-block", type=int, default=0)
+    a = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # host-side barrier / max only (no data-path collective)
+        dist.init_process_group("gloo")
+
+    gen_pat = a.pattern
+    prep = prepare(gen_pat)
+    dev = engine.get_device(local)
+    t0 = time.time()
+    plan = engine.Plan(dev, gen_pat, a.max_block)
+    plan.set_counts(prep["Mk"], prep["Uk"])
+    t_setup = time.time() - t0
+    groups = prep["groups"]
+
+    def step(s):
+        g = groups[(s * world + rank) % len(groups)]
+        plan.run([g])
+        return plan.stats()
+
+    for s in range(a.warmup):
+        step(s)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t_start = time.perf_counter()
+    stats = [step(a.warmup + s) for s in range(a.steps)]
+    t_end = time.perf_counter()
+    barrier()
+    elapsed = t_end - t_start
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    units_rank = sum(s["units"] for s in stats)
+    units = units_rank * world
+    dp_ms = sum(s["dp_ms"] for s in stats)
+    alg = sum(s["alg_bytes"] for s in stats)
+    achieved = alg / (dp_ms / 1e3) / 1e9
+    lanes = len(groups[0][3])
+    tr = committed_traffic(gen_pat, lanes)
+    if rank == 0:
+        ms_step = elapsed / a.steps * 1e3
+        passes_full_cv = math.ceil(len(groups) / world)
+        line = {
+            "metric": "patterns scored/sec (lattice cells x folds x (alpha,c)), 9-mer 5-fold CV 5x5 grid",
+            "value": units / elapsed,
+            "unit": "cell-scores/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 (scores, split sums) + f64 (single-pattern term); u32 counts",
+            "data": "synthetic",
+            "config": {"workload": f"synthetic 9-mer counts, general pattern {gen_pat} "
+                                   f"({plan.info['npat']} cells), 5x5 (alpha, c) grid, {NFOLDS}-fold CV; step = "
+                                   f"one (alpha, fold) group x {lanes} penalties over the whole lattice",
+                       "gen_pat": gen_pat, "cells": plan.info["npat"], "lanes_per_step": lanes,
+                       "units_per_step": plan.info["npat"] * lanes, "block_cells": plan.info["block"],
+                       "alphas": ALPHAS, "penalties": PENALTIES, "nfolds": NFOLDS},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS,
+                         "traffic": (tr["hbm_bytes_per_pass"] if tr else None)},
+            "dp_kernel_ms_per_step": dp_ms / a.steps,
+            "backtrack_ms_per_step": sum(s["backtrack_ms"] for s in stats) / a.steps,
+            "cv_5x5x5_wall_s": passes_full_cv * ms_step / 1e3,
+            "fold_split_s": prep["t_fold_s"],
+            "setup_s": t_setup,
+        }
+        if tr:
+            line["roofline"]["traffic_source"] = tr.get("source")
+        if not a.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(prep)
+        else:
+            line["cpu_baseline"] = None
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

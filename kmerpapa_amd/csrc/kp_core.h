@@ -75,6 +75,15 @@ struct kp_hpair {
     uint32_t pad_;
 };
 
+// one low cell in level order: what the level phase needs, in one 16-byte load
+struct kp_lowdesc {
+    uint16_t l;      // low cell index inside the block
+    uint16_t l1, l2; // children of its first split (count recurrence); 0xFFFF for k-mer-low cells
+    uint16_t kl;     // k-mer-low index (k-mer-low cells only)
+    uint32_t info;   // packed low digits (4 bits per position)
+    uint32_t pad_;
+};
+
 // ---------------------------------------------------------------------------
 // scoring arithmetic (float64, order of operations as in the reference)
 // ---------------------------------------------------------------------------
@@ -248,6 +257,70 @@ __host__ __device__ inline void kp_dp_cell(const kp_geom &g, const kp_postab *lo
 }
 
 // ---------------------------------------------------------------------------
+// one DP cell for NL lanes at once (lanes interleaved in LDS: st[cell * NL + lane]).
+// Positions and pairs are unrolled so every LDS read of the cell can issue at once.
+// code_out[lane] = KP_NONE when the gathered high-position winner stands (its code is
+// already in global memory), else the new argmin code.
+// ---------------------------------------------------------------------------
+template <int NL>
+__host__ __device__ inline void kp_dp_cell_lanes(const kp_geom &g, const kp_postab *lowtabs, uint32_t l,
+                                                 uint32_t lowinfo, float *st, const kp_single_ctx &sc, double alpha,
+                                                 double beta, const double *pen, uint32_t *code_out) {
+    float *row = st + (size_t)l * NL;
+    if (sc.kmer) {  // level 0 (CV :145-151 / Fit :106-114)
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
+            code_out[j] = KP_SINGLE;
+        }
+        return;
+    }
+    float lbest[NL];
+    uint32_t lcode[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        lbest[j] = __builtin_huge_valf();
+        lcode[j] = KP_NONE;
+    }
+    // cells of a wave share their split signature (kp_plan.h orders them so), hence
+    // these loops are uniform; all reads of one pair are independent LDS loads
+    for (int i = 0; i < g.t; ++i) {
+        const uint32_t d = kp_low_digit(lowinfo, i);
+        const kp_postab &T = lowtabs[i];
+        const uint32_t np = T.np[d];
+        const uint32_t cg = (uint32_t)g.cgl[i];
+        for (uint32_t p = 0; p < np; ++p) {
+            const float *r1 = st + (size_t)(l - (d - T.pa[d][p]) * cg) * NL;
+            const float *r2 = st + (size_t)(l - (d - T.pb[d][p]) * cg) * NL;
+#pragma unroll
+            for (int j = 0; j < NL; ++j) {
+                const float v = r1[j] + r2[j];
+                if (v < lbest[j]) {
+                    lbest[j] = v;
+                    lcode[j] = (uint32_t)((i << 3) | p);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+        float best = row[j];
+        uint32_t code = KP_NONE;
+        if (lcode[j] != KP_NONE && !(best < lbest[j])) {  // low positions precede high ones in scan order
+            best = lbest[j];
+            code = lcode[j];
+        }
+        const double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
+        if (s < (double)best) {
+            best = (float)s;
+            code = KP_SINGLE;
+        }
+        row[j] = best;
+        code_out[j] = code;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // backtrack of one lane: DFS over the argmin tree from the root.
 // Returns the test -2LL of the root (CV :159-163) computed with the reference's f32
 // sums test[c1] + test[c2]; optionally lists leaves in reference order (Fit :17-24).
@@ -275,11 +348,9 @@ struct kp_frame {
     uint32_t st;
 };
 
-template <typename CT>
-__host__ __device__ inline float kp_backtrack_lane(const kp_geom &g, const kp_postab *tabs, const uint32_t *lowinfo_tab,
-                                                   const uint32_t *klofs, const uint16_t *kllist, const CT *K,
-                                                   const uint8_t *C, uint32_t lane, int fold, double alpha,
-                                                   double beta, uint64_t *leaves, uint64_t cap,
+template <typename LeafFn>
+__host__ __device__ inline float kp_backtrack_lane(const kp_geom &g, const kp_postab *tabs, const uint8_t *C,
+                                                   uint32_t lane, LeafFn leaf, uint64_t *leaves, uint64_t cap,
                                                    uint64_t *nleaves, uint32_t *bad) {
     kp_frame stk[KP_MAXDEPTH];
     int sp = 1;
@@ -296,7 +367,7 @@ __host__ __device__ inline float kp_backtrack_lane(const kp_geom &g, const kp_po
             uint32_t code = C[kp_lane_row(g, h, lane) + l];
             if (code == KP_SINGLE || code == KP_NONE) {
                 if (code == KP_NONE) err = 1;
-                ret = kp_leaf_test<CT>(g, tabs, lowinfo_tab, klofs, kllist, K, f.x, fold, alpha, beta);
+                ret = leaf(f.x);
                 if (leaves && nl < cap) leaves[nl] = f.x;
                 ++nl;
                 --sp;

@@ -28,7 +28,7 @@
 #include "kp_core.h"
 #include "kp_plan.h"
 
-#define KP_DP_THREADS 256
+#define KP_DP_MAX_THREADS 1024
 
 // ---------------------------------------------------------------------------
 // kernels
@@ -42,6 +42,8 @@ struct kp_dev_tables {
     const uint32_t *klofs;
     const uint16_t *kllist;
     const uint32_t *hlist;
+    const kp_lowdesc *ldesc;
+    const uint16_t *kl2l;
 };
 
 template <typename CT>
@@ -90,117 +92,211 @@ struct kp_dp_params {
     uint64_t hbase;
     int H;
     int lmax;
+    int dbg;  // timing ablation only (KP_DEBUG_SKIP): 1 = skip gather, 2 = skip level phase, 4 = skip logs
 };
 
-template <typename CT>
-__global__ void __launch_bounds__(KP_DP_THREADS) kp_dp_kernel(kp_dp_params P) {
+// first-min update of one float4 of candidates (strict "<": the earlier pair keeps ties)
+__device__ inline void kp_min4(float4 &best, uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, const float4 a,
+                               const float4 b, uint32_t code) {
+    float v;
+    v = a.x + b.x; if (v < best.x) { best.x = v; c0 = code; }
+    v = a.y + b.y; if (v < best.y) { best.y = v; c1 = code; }
+    v = a.z + b.z; if (v < best.z) { best.z = v; c2 = code; }
+    v = a.w + b.w; if (v < best.w) { best.w = v; c3 = code; }
+}
+
+#define KP_IPT 4  // low cells per thread per level (host checks level sizes)
+
+template <typename CT, int NL>
+__global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const kp_geom &g = P.g;
     const uint64_t h = P.T.hlist[P.hbase + blockIdx.x];
     const kp_group_dev *G = P.groups + blockIdx.y;
-    const int nl = G->nl;
     const uint32_t lane0 = (uint32_t)G->lane0;
     const int fold = G->fold;
     const double alpha = G->alpha, beta = G->beta;
     const uint32_t Bpad = g.Bpad;
+    double pen[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
 
-    // LDS carve-up: st[nl][Bpad] f32 | kc[n_kl] | hp[] | lowtabs[t] | ch[nl][Bpad] u8
+    // LDS: st[Bpad][NL] f32 (lanes interleaved) | cm[Bpad] CT | cu[Bpad] CT | hp[] | lowtabs[t]
     float *st = reinterpret_cast<float *>(smem);
-    kp_cnt *kc = reinterpret_cast<kp_cnt *>(smem + (size_t)nl * Bpad * 4);
-    kp_hpair *hp = reinterpret_cast<kp_hpair *>(reinterpret_cast<unsigned char *>(kc) + (size_t)g.n_kl * sizeof(kp_cnt));
-    kp_postab *lowtabs = reinterpret_cast<kp_postab *>(reinterpret_cast<unsigned char *>(hp) +
-                                                       (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair));
-    uint8_t *ch = reinterpret_cast<uint8_t *>(lowtabs) + (size_t)g.t * sizeof(kp_postab);
+    CT *cm = reinterpret_cast<CT *>(smem + (size_t)NL * Bpad * 4);
+    CT *cu = cm + Bpad;
+    kp_hpair *hp = reinterpret_cast<kp_hpair *>(cu + Bpad);
+    kp_postab *lowtabs = reinterpret_cast<kp_postab *>(hp + (g.kh * 7 + 1));
+
     const CT *K = reinterpret_cast<const CT *>(P.K);
-    const int np = kp_high_pair_count(g, P.T.tabs, h);  // wave-uniform
-    if (threadIdx.x == 0) kp_high_pairs(g, P.T.tabs, h, hp);
+    const int np = (P.dbg & 1) ? 0 : kp_high_pair_count(g, P.T.tabs, h);  // wave-uniform
+    const uint64_t rowstride = (uint64_t)g.Ltot * Bpad;
+    if (threadIdx.x == 0) {
+        kp_high_pairs(g, P.T.tabs, h, hp);
+        for (int p = 0; p < np; ++p) {  // child rows as element offsets of lane 0
+            hp[p].h1 *= rowstride;
+            hp[p].h2 *= rowstride;
+        }
+    }
     {
         const uint32_t *src = reinterpret_cast<const uint32_t *>(P.T.tabs);
         uint32_t *dst = reinterpret_cast<uint32_t *>(lowtabs);
         const uint32_t words = (uint32_t)g.t * (uint32_t)(sizeof(kp_postab) / 4);
         for (uint32_t e = threadIdx.x; e < words; e += blockDim.x) dst[e] = src[e];
     }
-    for (uint32_t kl = threadIdx.x; kl < g.n_kl; kl += blockDim.x) kc[kl] = kp_kl_counts<CT>(g, K, h, kl, fold);
+    // train counts of the block's k-mer-low cells; the level loop aggregates the rest
+    for (uint32_t kl = threadIdx.x; kl < g.n_kl; kl += blockDim.x) {
+        const kp_cnt c = kp_kl_counts<CT>(g, K, h, kl, fold);
+        const uint32_t l = P.T.kl2l[kl];
+        cm[l] = (CT)c.mtr;
+        cu[l] = (CT)c.utr;
+    }
     __syncthreads();
 
     // ---- phase 1: high-position splits, gathered as whole child-block rows ----
+    // winner value -> LDS (interleaved), winner code -> global C directly
     const uint32_t nch = Bpad / 4;
-    for (uint32_t item = threadIdx.x; item < (uint32_t)nl * nch; item += blockDim.x) {
+    for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
         const uint32_t ll = item / nch, c = item % nch;
-        const uint32_t lane = lane0 + ll;
+        const uint64_t lrow = (uint64_t)(lane0 + ll) * Bpad + 4 * c;
+        const float *base = P.S + lrow;
         float4 best = make_float4(__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf(),
                                   __builtin_huge_valf());
         uint32_t c0 = KP_NONE, c1 = KP_NONE, c2 = KP_NONE, c3 = KP_NONE;
         int p = 0;
-        for (; p + 2 <= np; p += 2) {
-            const float4 a0 = *reinterpret_cast<const float4 *>(P.S + kp_lane_row(g, hp[p].h1, lane) + 4 * c);
-            const float4 b0 = *reinterpret_cast<const float4 *>(P.S + kp_lane_row(g, hp[p].h2, lane) + 4 * c);
-            const float4 a1 = *reinterpret_cast<const float4 *>(P.S + kp_lane_row(g, hp[p + 1].h1, lane) + 4 * c);
-            const float4 b1 = *reinterpret_cast<const float4 *>(P.S + kp_lane_row(g, hp[p + 1].h2, lane) + 4 * c);
-            const uint32_t k0 = hp[p].code, k1 = hp[p + 1].code;
-            float v;
-            v = a0.x + b0.x; if (v < best.x) { best.x = v; c0 = k0; }
-            v = a0.y + b0.y; if (v < best.y) { best.y = v; c1 = k0; }
-            v = a0.z + b0.z; if (v < best.z) { best.z = v; c2 = k0; }
-            v = a0.w + b0.w; if (v < best.w) { best.w = v; c3 = k0; }
-            v = a1.x + b1.x; if (v < best.x) { best.x = v; c0 = k1; }
-            v = a1.y + b1.y; if (v < best.y) { best.y = v; c1 = k1; }
-            v = a1.z + b1.z; if (v < best.z) { best.z = v; c2 = k1; }
-            v = a1.w + b1.w; if (v < best.w) { best.w = v; c3 = k1; }
+        for (; p + 4 <= np; p += 4) {
+            const float4 a0 = *reinterpret_cast<const float4 *>(base + hp[p].h1);
+            const float4 b0 = *reinterpret_cast<const float4 *>(base + hp[p].h2);
+            const float4 a1 = *reinterpret_cast<const float4 *>(base + hp[p + 1].h1);
+            const float4 b1 = *reinterpret_cast<const float4 *>(base + hp[p + 1].h2);
+            const float4 a2 = *reinterpret_cast<const float4 *>(base + hp[p + 2].h1);
+            const float4 b2 = *reinterpret_cast<const float4 *>(base + hp[p + 2].h2);
+            const float4 a3 = *reinterpret_cast<const float4 *>(base + hp[p + 3].h1);
+            const float4 b3 = *reinterpret_cast<const float4 *>(base + hp[p + 3].h2);
+            kp_min4(best, c0, c1, c2, c3, a0, b0, hp[p].code);
+            kp_min4(best, c0, c1, c2, c3, a1, b1, hp[p + 1].code);
+            kp_min4(best, c0, c1, c2, c3, a2, b2, hp[p + 2].code);
+            kp_min4(best, c0, c1, c2, c3, a3, b3, hp[p + 3].code);
         }
         for (; p < np; ++p) {
-            const float4 a0 = *reinterpret_cast<const float4 *>(P.S + kp_lane_row(g, hp[p].h1, lane) + 4 * c);
-            const float4 b0 = *reinterpret_cast<const float4 *>(P.S + kp_lane_row(g, hp[p].h2, lane) + 4 * c);
-            const uint32_t k0 = hp[p].code;
-            float v;
-            v = a0.x + b0.x; if (v < best.x) { best.x = v; c0 = k0; }
-            v = a0.y + b0.y; if (v < best.y) { best.y = v; c1 = k0; }
-            v = a0.z + b0.z; if (v < best.z) { best.z = v; c2 = k0; }
-            v = a0.w + b0.w; if (v < best.w) { best.w = v; c3 = k0; }
+            const float4 a0 = *reinterpret_cast<const float4 *>(base + hp[p].h1);
+            const float4 b0 = *reinterpret_cast<const float4 *>(base + hp[p].h2);
+            kp_min4(best, c0, c1, c2, c3, a0, b0, hp[p].code);
         }
-        *reinterpret_cast<float4 *>(st + (size_t)ll * Bpad + 4 * c) = best;
-        *reinterpret_cast<uint32_t *>(ch + (size_t)ll * Bpad + 4 * c) = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+        float *sl = st + (size_t)(4 * c) * NL + ll;
+        sl[0] = best.x;
+        sl[NL] = best.y;
+        sl[2 * NL] = best.z;
+        sl[3 * NL] = best.w;
+        *reinterpret_cast<uint32_t *>(P.C + h * rowstride + lrow) = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
     }
     __syncthreads();
 
     // ---- phase 2: low levels inside the block ----
+    // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
+    // the next level's descriptors are loaded while the current level computes
     const bool high_zero = (P.H == 0);
-    for (int lam = 0; lam <= P.lmax; ++lam) {
-        const int beg = P.T.loff[lam];
-        const uint32_t cnt = (uint32_t)(P.T.loff[lam + 1] - beg);
-        for (uint32_t item = threadIdx.x; item < (uint32_t)nl * cnt; item += blockDim.x) {
-            const uint32_t ll = item / cnt, q = item % cnt;
-            const uint32_t l = P.T.lorder[beg + q];
-            const uint32_t info = P.T.lowinfo[l];
-            kp_single_ctx sc;
-            sc.kmer = high_zero && lam == 0;
-            kp_cnt c = {0, 0, 0, 0};
-            for (uint32_t e = P.T.klofs[l]; e < P.T.klofs[l + 1]; ++e) {
-                const kp_cnt &x = kc[P.T.kllist[e]];
-                c.mtr += x.mtr; c.utr += x.utr; c.mte += x.mte; c.ute += x.ute;
+    const int lmax = (P.dbg & 2) ? -1 : P.lmax;
+    const uint4 *desc = reinterpret_cast<const uint4 *>(P.T.ldesc);
+    uint4 cur[KP_IPT], nxt[KP_IPT];
+    {
+        const int beg = P.T.loff[0], cnt = P.T.loff[1] - beg;
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) {
+            const int q = (int)threadIdx.x + k * (int)blockDim.x;
+            if (q < cnt) cur[k] = desc[beg + q];
+        }
+    }
+    uint8_t *Cb = P.C + h * rowstride + (uint64_t)lane0 * Bpad;
+    for (int lam = 0; lam <= lmax; ++lam) {
+        const int beg = P.T.loff[lam], cnt = P.T.loff[lam + 1] - beg;
+        if (lam < lmax) {
+            const int nbeg = P.T.loff[lam + 1], ncnt = P.T.loff[lam + 2] - nbeg;
+#pragma unroll
+            for (int k = 0; k < KP_IPT; ++k) {
+                const int q = (int)threadIdx.x + k * (int)blockDim.x;
+                if (q < ncnt) nxt[k] = desc[nbeg + q];
             }
-            sc.c = c;
-            if (!sc.kmer) {
-                const double p = kp_rate(c, alpha, beta);
-                sc.logp = log(p);
-                sc.log1mp = log(1.0 - p);
-            } else {
+        }
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) {
+            const int q = (int)threadIdx.x + k * (int)blockDim.x;
+            if (q < cnt) {
+                const uint32_t l = cur[k].x & 0xFFFFu;
+                const uint32_t l1 = cur[k].x >> 16, l2 = cur[k].y & 0xFFFFu;
+                const uint32_t info = cur[k].z;
+                CT mt, ut;
+                if (lam == 0) {
+                    mt = cm[l];
+                    ut = cu[l];
+                } else {
+                    // count recurrence on the first split (the reference's M_mem/U_mem rows)
+                    mt = cm[l1] + cm[l2];
+                    ut = cu[l1] + cu[l2];
+                    cm[l] = mt;
+                    cu[l] = ut;
+                }
+                kp_single_ctx sc;
+                sc.kmer = high_zero && lam == 0;
+                sc.c.mtr = (uint64_t)mt;
+                sc.c.utr = (uint64_t)ut;
+                sc.c.mte = sc.c.ute = 0;
                 sc.logp = sc.log1mp = 0.0;
+                if (!sc.kmer && !(P.dbg & 4)) {
+                    const double pr = kp_rate(sc.c, alpha, beta);
+                    sc.logp = log(pr);
+                    sc.log1mp = log(1.0 - pr);
+                }
+                uint32_t code[NL];
+                kp_dp_cell_lanes<NL>(g, lowtabs, l, info, st, sc, alpha, beta, pen, code);
+#pragma unroll
+                for (int j = 0; j < NL; ++j)
+                    if (code[j] != KP_NONE) Cb[(uint64_t)j * Bpad + l] = (uint8_t)code[j];
             }
-            kp_dp_cell(g, lowtabs, l, info, st + (size_t)ll * Bpad, ch + (size_t)ll * Bpad, sc, alpha, beta, G->pen[ll]);
         }
         __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) cur[k] = nxt[k];
     }
 
-    // ---- phase 3: store the block ----
-    for (uint32_t item = threadIdx.x; item < (uint32_t)nl * nch; item += blockDim.x) {
+    // ---- phase 3: store the block's train rows ----
+    for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
         const uint32_t ll = item / nch, c = item % nch;
-        const uint64_t row = kp_lane_row(g, h, lane0 + ll);
-        *reinterpret_cast<float4 *>(P.S + row + 4 * c) = *reinterpret_cast<const float4 *>(st + (size_t)ll * Bpad + 4 * c);
-        *reinterpret_cast<uint32_t *>(P.C + row + 4 * c) = *reinterpret_cast<const uint32_t *>(ch + (size_t)ll * Bpad + 4 * c);
+        const float *sl = st + (size_t)(4 * c) * NL + ll;
+        *reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c) =
+            make_float4(sl[0], sl[NL], sl[2 * NL], sl[3 * NL]);
     }
 }
 
+__device__ inline uint64_t kp_wave_sum(uint64_t v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// test -2LL of a leaf cell: the wave splits the leaf's k-mer-low rows, then reduces
+template <typename CT>
+__device__ inline float kp_leaf_test_wave(const kp_geom &g, const kp_dev_tables &T, const CT *K, uint64_t x, int fold,
+                                          double alpha, double beta) {
+    const uint64_t h = x / g.B;
+    const uint32_t l = (uint32_t)(x % g.B);
+    const uint32_t b = T.klofs[l], e = T.klofs[l + 1];
+    uint64_t mtr = 0, utr = 0, mte = 0, ute = 0;
+    for (uint32_t q = b + (threadIdx.x & 63u); q < e; q += 64) {
+        const kp_cnt c = kp_kl_counts<CT>(g, K, h, T.kllist[q], fold);
+        mtr += c.mtr; utr += c.utr; mte += c.mte; ute += c.ute;
+    }
+    kp_cnt c;
+    c.mtr = kp_wave_sum(mtr);
+    c.utr = kp_wave_sum(utr);
+    c.mte = kp_wave_sum(mte);
+    c.ute = kp_wave_sum(ute);
+    if (fold < 0) return 0.0f;
+    if (kp_is_kmer(g, h, T.lowinfo[l])) return kp_kmer_test(c, alpha, beta);
+    const double p = kp_rate(c, alpha, beta);
+    return kp_single_test(c, log(p), log(1.0 - p));
+}
+
+// one wave per lane: the DFS runs in lockstep in all 64 threads (uniform control flow)
 template <typename CT>
 __global__ void __launch_bounds__(64) kp_backtrack_kernel(kp_geom g, kp_dev_tables T, const CT *K, const float *S,
                                                           const uint8_t *C, const kp_group_dev *groups,
@@ -208,16 +304,21 @@ __global__ void __launch_bounds__(64) kp_backtrack_kernel(kp_geom g, kp_dev_tabl
                                                           float *root_test, uint64_t *nleaves, uint32_t *bad,
                                                           uint64_t *leaves, uint64_t cap) {
     const uint32_t lane = blockIdx.x;
-    if (threadIdx.x != 0) return;
     const kp_group_dev *G = groups + lanegrp[lane];
-    root_train[lane] = S[kp_lane_row(g, g.nblocks - 1, lane) + (g.B - 1)];
+    const int fold = G->fold;
+    const double alpha = G->alpha, beta = G->beta;
     uint64_t n = 0;
     uint32_t err = 0;
-    float t = kp_backtrack_lane<CT>(g, T.tabs, T.lowinfo, T.klofs, T.kllist, K, C, lane, G->fold, G->alpha, G->beta,
-                                    leaves ? leaves + (uint64_t)lane * cap : nullptr, cap, &n, &err);
-    root_test[lane] = t;
-    nleaves[lane] = n;
-    bad[lane] = err;
+    auto leaf = [&](uint64_t x) { return kp_leaf_test_wave<CT>(g, T, K, x, fold, alpha, beta); };
+    const bool writer = threadIdx.x == 0;
+    float t = kp_backtrack_lane(g, T.tabs, C, lane, leaf, writer && leaves ? leaves + (uint64_t)lane * cap : nullptr,
+                                cap, &n, &err);
+    if (writer) {
+        root_train[lane] = S[kp_lane_row(g, g.nblocks - 1, lane) + (g.B - 1)];
+        root_test[lane] = t;
+        nleaves[lane] = n;
+        bad[lane] = err;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -256,6 +357,8 @@ struct kp_plan {
     uint32_t *d_klofs = nullptr;
     uint16_t *d_kllist = nullptr;
     uint32_t *d_hlist = nullptr;
+    kp_lowdesc *d_ldesc = nullptr;
+    uint16_t *d_kl2l = nullptr;
     // counts
     void *d_K = nullptr;
     int nf = 0;
@@ -284,6 +387,8 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     T.klofs = p->d_klofs;
     T.kllist = p->d_kllist;
     T.hlist = p->d_hlist;
+    T.ldesc = p->d_ldesc;
+    T.kl2l = p->d_kl2l;
     return T;
 }
 
@@ -359,7 +464,8 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
     if ((rc = upload(p, &p->d_tabs, p->hp.tabs)) || (rc = upload(p, &p->d_lowinfo, p->hp.lowinfo)) ||
         (rc = upload(p, &p->d_lorder, p->hp.lorder)) || (rc = upload(p, &p->d_loff, p->hp.loff)) ||
         (rc = upload(p, &p->d_klofs, p->hp.klofs)) || (rc = upload(p, &p->d_kllist, p->hp.kllist)) ||
-        (rc = upload(p, &p->d_hlist, p->hp.hlist))) {
+        (rc = upload(p, &p->d_hlist, p->hp.hlist)) || (rc = upload(p, &p->d_ldesc, p->hp.ldesc)) ||
+        (rc = upload(p, &p->d_kl2l, p->hp.kl2l))) {
         kp_plan_destroy(p);
         return rc;
     }
@@ -371,6 +477,7 @@ void kp_plan_destroy(kp_plan *p) {
     if (!p) return;
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
     void *bufs[] = {p->d_tabs, p->d_lowinfo, p->d_lorder, p->d_loff, p->d_klofs, p->d_kllist, p->d_hlist,
+                    p->d_ldesc, p->d_kl2l,
                     p->d_K, p->d_S, p->d_C, p->d_groups, p->d_lanegrp, p->d_rtrain, p->d_rtest,
                     p->d_nleaves, p->d_bad, p->d_leaves};
     for (void *b : bufs) dfree(b);
@@ -454,10 +561,42 @@ int kp_set_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers, in
 
 }  // extern "C"
 
-static size_t dp_lds_bytes(const kp::host_plan &hp, int nl) {
+static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
     const kp_geom &g = hp.g;
-    return (size_t)nl * g.Bpad * 5 + (size_t)g.n_kl * sizeof(kp_cnt) + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) +
+    return (size_t)nl * g.Bpad * 4 + 2 * (size_t)g.Bpad * ct_bytes + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) +
            (size_t)g.t * sizeof(kp_postab) + 16;
+}
+
+template <typename CT, int NL>
+static int launch_dp(kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
+    if (lds > 65536)
+        KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_kernel<CT, NL>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((kp_dp_kernel<CT, NL>), dim3(nb, ngroups), dim3(threads), lds, c->stream, P);
+    KP_HIP(hipGetLastError());
+    return KP_OK;
+}
+
+template <typename CT>
+static int launch_dp_nl(int nl, kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads,
+                        size_t lds) {
+    switch (nl) {
+        case 1: return launch_dp<CT, 1>(c, P, nb, ngroups, threads, lds);
+        case 2: return launch_dp<CT, 2>(c, P, nb, ngroups, threads, lds);
+        case 3: return launch_dp<CT, 3>(c, P, nb, ngroups, threads, lds);
+        case 4: return launch_dp<CT, 4>(c, P, nb, ngroups, threads, lds);
+        case 5: return launch_dp<CT, 5>(c, P, nb, ngroups, threads, lds);
+        case 6: return launch_dp<CT, 6>(c, P, nb, ngroups, threads, lds);
+        case 7: return launch_dp<CT, 7>(c, P, nb, ngroups, threads, lds);
+        case 8: return launch_dp<CT, 8>(c, P, nb, ngroups, threads, lds);
+    }
+    return fail(KP_E_ARG, "lanes per workgroup must be 1..8");
+}
+
+static int dp_threads() {
+    const char *e = getenv("KP_DP_THREADS");
+    int v = e ? atoi(e) : 256;
+    return (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) ? v : 256;
 }
 
 static int lanes_per_wg_default() {
@@ -476,8 +615,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     g.nf = p->nf;
     // split user groups into device groups that fit the LDS budget
     int per_wg = lanes_per_wg_default();
-    while (per_wg > 1 && dp_lds_bytes(hp, per_wg) > c->lds_max) --per_wg;
-    if (dp_lds_bytes(hp, 1) > c->lds_max) return fail(KP_E_ARG, "block does not fit LDS");
+    while (per_wg > 1 && dp_lds_bytes(hp, per_wg, sizeof(CT)) > c->lds_max) --per_wg;
+    if (dp_lds_bytes(hp, 1, sizeof(CT)) > c->lds_max) return fail(KP_E_ARG, "block does not fit LDS");
     std::vector<kp_group_dev> dg;
     std::vector<uint32_t> lanegrp;
     uint32_t lane = 0;
@@ -501,6 +640,17 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     }
     const uint32_t Ltot = lane;
     g.Ltot = Ltot;
+    // launch classes: device groups with equal lane counts share one launch per level
+    std::stable_sort(dg.begin(), dg.end(), [](const kp_group_dev &a, const kp_group_dev &b) { return a.nl > b.nl; });
+    lanegrp.assign(Ltot, 0);
+    for (size_t i = 0; i < dg.size(); ++i)
+        for (int j = 0; j < dg[i].nl; ++j) lanegrp[dg[i].lane0 + j] = (uint32_t)i;
+    // threads per workgroup: every level of the block must fit KP_IPT cells per thread
+    int max_level_cells = 0;
+    for (int l = 0; l <= hp.lmax; ++l) max_level_cells = std::max(max_level_cells, hp.loff[l + 1] - hp.loff[l]);
+    int threads = dp_threads();
+    while (threads < KP_DP_MAX_THREADS && threads * KP_IPT < max_level_cells) threads *= 2;
+    if (threads * KP_IPT < max_level_cells) return fail(KP_E_ARG, "block level too wide for one workgroup");
     // lane storage
     if (Ltot > p->lanes_cap) {
         dfree(p->d_S);
@@ -543,9 +693,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.C = p->d_C;
     P.groups = p->d_groups;
     P.lmax = hp.lmax;
-    const size_t lds = dp_lds_bytes(hp, per_wg);
-    if (lds > 65536) KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_kernel<CT>),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    P.dbg = getenv("KP_DEBUG_SKIP") ? atoi(getenv("KP_DEBUG_SKIP")) : 0;
     KP_HIP(hipEventRecord(c->ev[0], c->stream));
     uint64_t launches = 0;
     for (int H = 0; H <= hp.hmax; ++H) {
@@ -553,13 +701,20 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         if (!nb) continue;
         P.hbase = hp.hoff[H];
         P.H = H;
-        hipLaunchKernelGGL(kp_dp_kernel<CT>, dim3((unsigned)nb, (unsigned)dg.size()), dim3(KP_DP_THREADS), lds,
-                           c->stream, P);
-        KP_HIP(hipGetLastError());
-        ++launches;
+        for (size_t i = 0; i < dg.size();) {
+            size_t j = i;
+            while (j < dg.size() && dg[j].nl == dg[i].nl) ++j;
+            kp_dp_params Q = P;
+            Q.groups = p->d_groups + i;
+            int rc = launch_dp_nl<CT>(dg[i].nl, c, Q, (unsigned)nb, (unsigned)(j - i), threads,
+                                      dp_lds_bytes(hp, dg[i].nl, sizeof(CT)));
+            if (rc) return rc;
+            ++launches;
+            i = j;
+        }
     }
     KP_HIP(hipEventRecord(c->ev[1], c->stream));
-    hipLaunchKernelGGL(kp_backtrack_kernel<CT>, dim3(Ltot), dim3(64), 0, c->stream, g, P.T,
+    if (!P.dbg) hipLaunchKernelGGL(kp_backtrack_kernel<CT>, dim3(Ltot), dim3(64), 0, c->stream, g, P.T,
                        reinterpret_cast<const CT *>(p->d_K), p->d_S, p->d_C, p->d_groups, p->d_lanegrp, p->d_rtrain,
                        p->d_rtest, p->d_nleaves, p->d_bad, p->d_leaves, (uint64_t)hp.n_kmers);
     KP_HIP(hipGetLastError());
@@ -576,7 +731,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     KP_HIP(hipEventElapsedTime(&dp_ms, c->ev[0], c->ev[1]));
     KP_HIP(hipEventElapsedTime(&bt_ms, c->ev[1], c->ev[2]));
     for (uint32_t i = 0; i < Ltot; ++i) {
-        if (bad[i]) return fail(KP_E_PARITY, "argmin tree of lane " + std::to_string(i) + " is broken");
+        if (bad[i] && !P.dbg) return fail(KP_E_PARITY, "argmin tree of lane " + std::to_string(i) + " is broken");
         if (root_train) root_train[i] = rtr[i];
         if (root_test) root_test[i] = rte[i];
         if (n_leaves) n_leaves[i] = nlv[i];

@@ -9,6 +9,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -41,6 +42,8 @@ struct host_plan {
     std::vector<uint32_t> lowinfo;     // [B] packed low digits
     std::vector<uint16_t> lorder;      // [B] low cells sorted by low level
     std::vector<int32_t> loff;         // [lmax + 2]
+    std::vector<kp_lowdesc> ldesc;     // [B] low cells in level order
+    std::vector<uint16_t> kl2l;        // [n_kl] k-mer-low index -> low cell
     std::vector<uint32_t> klofs;       // [B + 1]
     std::vector<uint16_t> kllist;      // k-mer-low cells matching each low cell
     std::vector<uint32_t> hlist;       // [nblocks] blocks sorted by high level
@@ -108,6 +111,7 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     }
     // low cells: digits, levels, order, matching k-mer-low cells
     uint32_t B = g.B;
+    if (B > 0xFFFFu) return "block too large for 16-bit cell ids";
     P.lowinfo.resize(B);
     std::vector<int> llev(B);
     int lmax = 0;
@@ -130,8 +134,49 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     for (int s = 0; s <= lmax; ++s) P.loff[s + 1] += P.loff[s];
     P.lorder.resize(B);
     {
-        std::vector<int32_t> fill(P.loff.begin(), P.loff.end() - 1);
-        for (uint32_t l = 0; l < B; ++l) P.lorder[fill[llev[l]]++] = (uint16_t)l;
+        // inside a level any order is valid (cells only read lower levels); cells are
+        // grouped by their split signature (pairs at each low position) so that the 64
+        // cells of a wave run the same pair loops (no divergence in the level phase)
+        std::vector<uint64_t> key(B);
+        for (uint32_t l = 0; l < B; ++l) {
+            uint64_t sig = 0;
+            for (int i = 0; i < t; ++i) sig = sig * 8 + P.tabs[i].np[kp_low_digit(P.lowinfo[l], i)];
+            key[l] = ((uint64_t)llev[l] << 48) | (sig << 16) | l;
+        }
+        std::vector<uint32_t> idx(B);
+        for (uint32_t l = 0; l < B; ++l) idx[l] = l;
+        std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+        for (uint32_t q = 0; q < B; ++q) P.lorder[q] = (uint16_t)idx[q];
+    }
+    // level-ordered descriptors: first split pair (count recurrence) and k-mer-low index
+    P.ldesc.resize(B);
+    P.kl2l.assign(nkl, 0);
+    for (uint32_t q = 0; q < B; ++q) {
+        uint32_t l = P.lorder[q];
+        kp_lowdesc D;
+        memset(&D, 0, sizeof(D));
+        D.l = (uint16_t)l;
+        D.info = P.lowinfo[l];
+        D.l1 = D.l2 = 0xFFFF;
+        if (llev[l] == 0) {
+            uint32_t kl = 0, w = 1;
+            for (int i = 0; i < t; ++i) {
+                kl += kp_low_digit(D.info, i) * w;
+                w *= g.n[i];
+            }
+            D.kl = (uint16_t)kl;
+            P.kl2l[kl] = (uint16_t)l;
+        } else {
+            for (int i = 0; i < t; ++i) {
+                uint32_t d = kp_low_digit(D.info, i);
+                if (P.tabs[i].np[d]) {
+                    D.l1 = (uint16_t)(l - (d - P.tabs[i].pa[d][0]) * (uint32_t)g.cgl[i]);
+                    D.l2 = (uint16_t)(l - (d - P.tabs[i].pb[d][0]) * (uint32_t)g.cgl[i]);
+                    break;
+                }
+            }
+        }
+        P.ldesc[q] = D;
     }
     // nucleotide index sets of every (position, digit): nucleotide c of code x has
     // k-mer digit = index of c in code[g] = perm digit of c (nucleotides come first)

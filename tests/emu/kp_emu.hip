@@ -17,6 +17,20 @@
 namespace {
 std::string g_err;
 
+void cell_lanes(int nl, const kp_geom &g, const kp_postab *tabs, uint32_t l, uint32_t info, float *st,
+                const kp_single_ctx &sc, double a, double b, const double *pen, uint32_t *code) {
+    switch (nl) {
+        case 1: kp_dp_cell_lanes<1>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+        case 2: kp_dp_cell_lanes<2>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+        case 3: kp_dp_cell_lanes<3>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+        case 4: kp_dp_cell_lanes<4>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+        case 5: kp_dp_cell_lanes<5>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+        case 6: kp_dp_cell_lanes<6>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+        case 7: kp_dp_cell_lanes<7>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+        default: kp_dp_cell_lanes<8>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+    }
+}
+
 template <typename CT>
 int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, const kp_group_dev *groups, int ngroups,
         float *root_train, float *root_test, uint64_t *nleaves, float *dump_score, uint8_t *dump_code,
@@ -64,17 +78,15 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
     std::vector<kp_hpair> hpairs(KP_MAX_HPAIRS);
     std::vector<kp_cnt> kc(g.n_kl);
     std::vector<float> st;
-    std::vector<uint8_t> ch;
     for (int H = 0; H <= hp.hmax; ++H) {
         for (uint64_t q = hp.hoff[H]; q < hp.hoff[H + 1]; ++q) {
             uint64_t h = hp.hlist[q];
             int np = kp_high_pairs(g, hp.tabs.data(), h, hpairs.data());
             for (int gi = 0; gi < ngroups; ++gi) {
                 const kp_group_dev &G = groups[gi];
-                st.assign((size_t)G.nl * g.Bpad, 0.0f);
-                ch.assign((size_t)G.nl * g.Bpad, 0);
+                st.assign((size_t)G.nl * g.Bpad, 0.0f);  // interleaved [cell][lane], like the kernel
                 for (uint32_t kl = 0; kl < g.n_kl; ++kl) kc[kl] = kp_kl_counts<CT>(g, K.data(), h, kl, G.fold);
-                // phase 1: gather
+                // phase 1: gather (value -> st, code -> global C)
                 for (int ll = 0; ll < G.nl; ++ll) {
                     uint32_t lane = (uint32_t)G.lane0 + ll;
                     for (uint32_t l = 0; l < g.Bpad; ++l) {
@@ -84,39 +96,45 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
                             float v = S[kp_lane_row(g, hpairs[p].h1, lane) + l] + S[kp_lane_row(g, hpairs[p].h2, lane) + l];
                             if (v < best) { best = v; code = hpairs[p].code; }
                         }
-                        st[(size_t)ll * g.Bpad + l] = best;
-                        ch[(size_t)ll * g.Bpad + l] = (uint8_t)code;
+                        st[(size_t)l * G.nl + ll] = best;
+                        C[kp_lane_row(g, h, lane) + l] = (uint8_t)code;
                     }
                 }
-                // phase 2: levels
+                // phase 2: levels (same descriptor table, count recurrence and cell function as kp_dp_kernel)
+                std::vector<CT> cm(g.Bpad, 0), cu(g.Bpad, 0);
+                for (uint32_t kl = 0; kl < g.n_kl; ++kl) {
+                    cm[hp.kl2l[kl]] = (CT)kc[kl].mtr;
+                    cu[hp.kl2l[kl]] = (CT)kc[kl].utr;
+                }
                 for (int lam = 0; lam <= hp.lmax; ++lam) {
-                    for (int ll = 0; ll < G.nl; ++ll) {
-                        for (int qq = hp.loff[lam]; qq < hp.loff[lam + 1]; ++qq) {
-                            uint32_t l = hp.lorder[qq];
-                            kp_single_ctx sc;
-                            sc.kmer = (H == 0 && lam == 0);
-                            kp_cnt c = {0, 0, 0, 0};
-                            for (uint32_t e = hp.klofs[l]; e < hp.klofs[l + 1]; ++e) {
-                                const kp_cnt &x = kc[hp.kllist[e]];
-                                c.mtr += x.mtr; c.utr += x.utr; c.mte += x.mte; c.ute += x.ute;
-                            }
-                            sc.c = c;
-                            sc.logp = sc.log1mp = 0.0;
-                            if (!sc.kmer) {
-                                double p = kp_rate(c, G.alpha, G.beta);
-                                sc.logp = log(p);
-                                sc.log1mp = log(1.0 - p);
-                            }
-                            kp_dp_cell(g, hp.tabs.data(), l, hp.lowinfo[l], st.data() + (size_t)ll * g.Bpad,
-                                       ch.data() + (size_t)ll * g.Bpad, sc, G.alpha, G.beta, G.pen[ll]);
+                    for (int qq = hp.loff[lam]; qq < hp.loff[lam + 1]; ++qq) {
+                        const kp_lowdesc &D = hp.ldesc[qq];
+                        uint32_t l = D.l;
+                        CT mt = lam == 0 ? cm[l] : (CT)(cm[D.l1] + cm[D.l2]);
+                        CT ut = lam == 0 ? cu[l] : (CT)(cu[D.l1] + cu[D.l2]);
+                        cm[l] = mt;
+                        cu[l] = ut;
+                        kp_single_ctx sc;
+                        sc.kmer = (H == 0 && lam == 0);
+                        sc.c.mtr = mt;
+                        sc.c.utr = ut;
+                        sc.c.mte = sc.c.ute = 0;
+                        sc.logp = sc.log1mp = 0.0;
+                        if (!sc.kmer) {
+                            double p = kp_rate(sc.c, G.alpha, G.beta);
+                            sc.logp = log(p);
+                            sc.log1mp = log(1.0 - p);
                         }
+                        uint32_t code[KP_GROUP_LANES];
+                        cell_lanes(G.nl, g, hp.tabs.data(), l, D.info, st.data(), sc, G.alpha, G.beta, G.pen, code);
+                        for (int j = 0; j < G.nl; ++j)
+                            if (code[j] != KP_NONE) C[kp_lane_row(g, h, (uint32_t)G.lane0 + j) + l] = (uint8_t)code[j];
                     }
                 }
                 // phase 3: store
                 for (int ll = 0; ll < G.nl; ++ll) {
                     uint64_t row = kp_lane_row(g, h, (uint32_t)G.lane0 + ll);
-                    memcpy(&S[row], &st[(size_t)ll * g.Bpad], g.Bpad * sizeof(float));
-                    memcpy(&C[row], &ch[(size_t)ll * g.Bpad], g.Bpad);
+                    for (uint32_t l = 0; l < g.Bpad; ++l) S[row + l] = st[(size_t)l * G.nl + ll];
                 }
             }
         }
@@ -129,10 +147,12 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
             root_train[lane] = S[kp_lane_row(g, g.nblocks - 1, lane) + g.B - 1];
             uint64_t n = 0;
             uint32_t bad = 0;
-            root_test[lane] = kp_backtrack_lane<CT>(g, hp.tabs.data(), hp.lowinfo.data(), hp.klofs.data(),
-                                                    hp.kllist.data(), K.data(), C.data(), lane, G.fold, G.alpha,
-                                                    G.beta, leaves ? leaves + lane * hp.n_kmers : nullptr,
-                                                    hp.n_kmers, &n, &bad);
+            auto leaf = [&](uint64_t x) {
+                return kp_leaf_test<CT>(g, hp.tabs.data(), hp.lowinfo.data(), hp.klofs.data(), hp.kllist.data(),
+                                        K.data(), x, G.fold, G.alpha, G.beta);
+            };
+            root_test[lane] = kp_backtrack_lane(g, hp.tabs.data(), C.data(), lane, leaf,
+                                                leaves ? leaves + lane * hp.n_kmers : nullptr, hp.n_kmers, &n, &bad);
             nleaves[lane] = n;
             if (bad) {
                 g_err = "broken argmin tree";
