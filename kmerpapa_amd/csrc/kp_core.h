@@ -203,70 +203,72 @@ __host__ __device__ inline uint64_t kp_lane_row(const kp_geom &g, uint64_t h, ui
     return (h * g.Ltot + lane) * (uint64_t)g.Bpad;
 }
 
-// ---------------------------------------------------------------------------
-// one DP cell of one lane, inside an LDS block
-//   st / ch : this lane's block row (train values / argmin codes), children final,
-//             own slot holding the best high-position candidate from the gather phase
-// ---------------------------------------------------------------------------
+// float64 single-pattern context of one cell, shared by every lane of a group
 struct kp_single_ctx {
     bool kmer;      // level-0 cell: reference uses the xlogy formula and no splits
     double logp, log1mp;
     kp_cnt c;
 };
 
-__host__ __device__ inline void kp_dp_cell(const kp_geom &g, const kp_postab *lowtabs, uint32_t l, uint32_t lowinfo,
-                                           float *st, uint8_t *ch, const kp_single_ctx &sc, double alpha,
-                                           double beta, double pen) {
-    float best = st[l];
-    uint32_t code = ch[l];
-    if (sc.kmer) {
-        // level 0 (CV :145-151 / Fit :106-114): the score is the k-mer's own term
-        st[l] = kp_kmer_train(sc.c, alpha, beta, pen);
-        ch[l] = (uint8_t)KP_SINGLE;
-        return;
+// ---------------------------------------------------------------------------
+// pair words: everything the level phase needs about the splits of one digit at one low
+// position, in one 64-bit load.  bits 8p..8p+3 = d - pa[d][p], bits 8p+4..8p+7 =
+// d - pb[d][p] (p < np <= 7, scan order), bits 56..63 = np.  Child of pair p at low
+// position i of cell l: l - delta * cgl[i].
+// ---------------------------------------------------------------------------
+__host__ __device__ inline uint64_t kp_pair_word(const kp_postab &T, uint32_t d) {
+    uint64_t w = (uint64_t)T.np[d] << 56;
+    for (uint32_t p = 0; p < T.np[d]; ++p)
+        w |= (uint64_t)(((d - T.pa[d][p]) & 15u) | (((d - T.pb[d][p]) & 15u) << 4)) << (8 * p);
+    return w;
+}
+
+// first-min over NP split pairs of one position for NL lanes; all 2*NP*NL LDS reads are
+// issued before the first compare (fully unrolled, no loop-carried dependence on loads)
+// 24-bit multiply (operands known < 2^24: one full-rate v_mul_u32_u24 on gfx950)
+__host__ __device__ inline uint32_t kp_mul24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
+
+// SP = pointer to the block's scores: float* on the host, an LDS (address space 3) pointer
+// in the kernels so every address is 32-bit
+template <int NL, int NP, typename SP>
+__host__ __device__ inline void kp_pairs_min(SP st, uint32_t l, uint32_t cg, uint64_t w, uint32_t code0,
+                                             float *lbest, uint32_t *lcode) {
+    float va[NP][NL], vb[NP][NL];
+    const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const uint32_t wp = (p < 4) ? (w0 >> (8 * p)) : (w1 >> (8 * (p - 4)));
+        const uint32_t l1 = l - kp_mul24(wp & 15u, cg);
+        const uint32_t l2 = l - kp_mul24((wp >> 4) & 15u, cg);
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            va[p][j] = st[l1 * NL + j];
+            vb[p][j] = st[l2 * NL + j];
+        }
     }
-    // low positions first in scan order
-    float lbest = __builtin_huge_valf();
-    uint32_t lcode = KP_NONE;
-    for (int i = 0; i < g.t; ++i) {
-        uint32_t d = kp_low_digit(lowinfo, i);
-        const kp_postab &T = lowtabs[i];
-        uint32_t cg = (uint32_t)g.cgl[i];
-        for (int j = 0; j < T.np[d]; ++j) {
-            uint32_t l1 = l - (d - T.pa[d][j]) * cg;
-            uint32_t l2 = l - (d - T.pb[d][j]) * cg;
-            float v = st[l1] + st[l2];
-            if (v < lbest) {
-                lbest = v;
-                lcode = (uint32_t)((i << 3) | j);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int j = 0; j < NL; ++j) {
+            const float v = va[p][j] + vb[p][j];
+            if (v < lbest[j]) {
+                lbest[j] = v;
+                lcode[j] = code0 | (uint32_t)p;
             }
         }
     }
-    // sequential-scan equivalence: a low candidate wins unless a high one is strictly lower
-    if (lcode != KP_NONE && !(best < lbest)) {
-        best = lbest;
-        code = lcode;
-    }
-    double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen);
-    if (s < (double)best) {
-        best = (float)s;
-        code = KP_SINGLE;
-    }
-    st[l] = best;
-    ch[l] = (uint8_t)code;
 }
 
 // ---------------------------------------------------------------------------
 // one DP cell for NL lanes at once (lanes interleaved in LDS: st[cell * NL + lane]).
-// Positions and pairs are unrolled so every LDS read of the cell can issue at once.
-// code_out[lane] = KP_NONE when the gathered high-position winner stands (its code is
-// already in global memory), else the new argmin code.
+// pw = pair words [t][16] (kp_pair_word).  code_out[lane] = KP_NONE when the gathered
+// high-position winner stands (its code is already stored), else the new argmin code.
 // ---------------------------------------------------------------------------
-template <int NL>
-__host__ __device__ inline void kp_dp_cell_lanes(const kp_geom &g, const kp_postab *lowtabs, uint32_t l,
-                                                 uint32_t lowinfo, float *st, const kp_single_ctx &sc, double alpha,
-                                                 double beta, const double *pen, uint32_t *code_out) {
-    float *row = st + (size_t)l * NL;
+template <int NL, typename SP, typename WP>
+__host__ __device__ inline void kp_dp_cell_lanes(const kp_geom &g, WP pw, uint32_t l, uint32_t lowinfo, SP st,
+                                                 const kp_single_ctx &sc, double alpha, double beta, const double *pen,
+                                                 uint32_t *code_out) {
+    SP row = st + l * NL;
     if (sc.kmer) {  // level 0 (CV :145-151 / Fit :106-114)
 #pragma unroll
         for (int j = 0; j < NL; ++j) {
@@ -282,22 +284,35 @@ __host__ __device__ inline void kp_dp_cell_lanes(const kp_geom &g, const kp_post
         lbest[j] = __builtin_huge_valf();
         lcode[j] = KP_NONE;
     }
-    // cells of a wave share their split signature (kp_plan.h orders them so), hence
-    // these loops are uniform; all reads of one pair are independent LDS loads
-    for (int i = 0; i < g.t; ++i) {
-        const uint32_t d = kp_low_digit(lowinfo, i);
-        const kp_postab &T = lowtabs[i];
-        const uint32_t np = T.np[d];
-        const uint32_t cg = (uint32_t)g.cgl[i];
-        for (uint32_t p = 0; p < np; ++p) {
-            const float *r1 = st + (size_t)(l - (d - T.pa[d][p]) * cg) * NL;
-            const float *r2 = st + (size_t)(l - (d - T.pb[d][p]) * cg) * NL;
+    // one pair word per low position, all loaded up front
+    uint64_t w[KP_MAXT];
 #pragma unroll
-            for (int j = 0; j < NL; ++j) {
-                const float v = r1[j] + r2[j];
-                if (v < lbest[j]) {
-                    lbest[j] = v;
-                    lcode[j] = (uint32_t)((i << 3) | p);
+    for (int i = 0; i < KP_MAXT; ++i) w[i] = (i < g.t) ? pw[i * 16 + kp_low_digit(lowinfo, i)] : 0;
+    // positions in scan order; np is 0, 1, 3 or 7 for every IUPAC code and, because cells
+    // of a wave share their split signature (kp_plan.h), nearly always wave-uniform
+#pragma unroll
+    for (int i = 0; i < KP_MAXT; ++i) {
+        if (i >= g.t) continue;
+        const uint32_t np = (uint32_t)(w[i] >> 56);
+        const uint32_t cg = (uint32_t)g.cgl[i] & 0xFFFFu;  // low place values are < 2^16 (block <= 65535)
+        const uint32_t code0 = (uint32_t)i << 3;
+        if (np == 1) {
+            kp_pairs_min<NL, 1>(st, l, cg, w[i], code0, lbest, lcode);
+        } else if (np == 3) {
+            kp_pairs_min<NL, 3>(st, l, cg, w[i], code0, lbest, lcode);
+        } else if (np == 7) {
+            kp_pairs_min<NL, 7>(st, l, cg, w[i], code0, lbest, lcode);
+        } else {
+            for (uint32_t p = 0; p < np; ++p) {  // not produced by the IUPAC tables; kept general
+                const uint32_t l1 = l - (uint32_t)((w[i] >> (8 * p)) & 15u) * cg;
+                const uint32_t l2 = l - (uint32_t)((w[i] >> (8 * p + 4)) & 15u) * cg;
+#pragma unroll
+                for (int j = 0; j < NL; ++j) {
+                    const float v = st[l1 * NL + j] + st[l2 * NL + j];
+                    if (v < lbest[j]) {
+                        lbest[j] = v;
+                        lcode[j] = code0 | p;
+                    }
                 }
             }
         }

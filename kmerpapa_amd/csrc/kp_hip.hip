@@ -30,6 +30,10 @@
 
 #define KP_DP_MAX_THREADS 1024
 
+// LDS-qualified element types: pointers to them are 32-bit and address LDS directly
+typedef __attribute__((address_space(3))) float kp_lds_f32;
+typedef __attribute__((address_space(3))) uint64_t kp_lds_u64;
+
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
@@ -44,6 +48,7 @@ struct kp_dev_tables {
     const uint32_t *hlist;
     const kp_lowdesc *ldesc;
     const uint16_t *kl2l;
+    const uint64_t *pw;
 };
 
 template <typename CT>
@@ -92,7 +97,9 @@ struct kp_dp_params {
     uint64_t hbase;
     int H;
     int lmax;
-    int dbg;  // timing ablation only (KP_DEBUG_SKIP): 1 = skip gather, 2 = skip level phase, 4 = skip logs
+    int remap;  // 1 = XCD-contiguous block order (KP_XCD_REMAP=1; measured 4% slower, off by default)
+    int dbg;  // timing ablation only (KP_DEBUG_SKIP, wrong results): 1 = skip gather, 2 = skip level phase,
+              // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier, 32 = no count recurrence
 };
 
 // first-min update of one float4 of candidates (strict "<": the earlier pair keeps ties)
@@ -105,13 +112,20 @@ __device__ inline void kp_min4(float4 &best, uint32_t &c0, uint32_t &c1, uint32_
     v = a.w + b.w; if (v < best.w) { best.w = v; c3 = code; }
 }
 
-#define KP_IPT 4  // low cells per thread per level (host checks level sizes)
+#define KP_IPT 2  // low cells per thread per level (host checks level sizes)
 
 template <typename CT, int NL>
 __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const kp_geom &g = P.g;
-    const uint64_t h = P.T.hlist[P.hbase + blockIdx.x];
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so give each XCD a
+    // contiguous run of the level's block list (neighbouring blocks share child rows in L2)
+    uint32_t widx = blockIdx.x;
+    if (P.remap) {
+        const uint32_t nb = gridDim.x, q = nb >> 3, r = nb & 7u, x = blockIdx.x & 7u;
+        widx = x * q + (x < r ? x : r) + (blockIdx.x >> 3);
+    }
+    const uint64_t h = P.T.hlist[P.hbase + widx];
     const kp_group_dev *G = P.groups + blockIdx.y;
     const uint32_t lane0 = (uint32_t)G->lane0;
     const int fold = G->fold;
@@ -121,12 +135,14 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
 #pragma unroll
     for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
 
-    // LDS: st[Bpad][NL] f32 (lanes interleaved) | cm[Bpad] CT | cu[Bpad] CT | hp[] | lowtabs[t]
+    // LDS: st[Bpad][NL] f32 (lanes interleaved) | cd[NL][Bpad] u8 argmin codes | cm[Bpad] CT | cu[Bpad] CT |
+    //      hp[] | pw[t][16]   (Bpad is a multiple of 16, so every carve stays 16-byte aligned)
     float *st = reinterpret_cast<float *>(smem);
-    CT *cm = reinterpret_cast<CT *>(smem + (size_t)NL * Bpad * 4);
+    uint8_t *cd = smem + (size_t)NL * Bpad * 4;
+    CT *cm = reinterpret_cast<CT *>(cd + (size_t)NL * Bpad);
     CT *cu = cm + Bpad;
     kp_hpair *hp = reinterpret_cast<kp_hpair *>(cu + Bpad);
-    kp_postab *lowtabs = reinterpret_cast<kp_postab *>(hp + (g.kh * 7 + 1));
+    uint64_t *pw = reinterpret_cast<uint64_t *>(hp + (g.kh * 7 + 1));
 
     const CT *K = reinterpret_cast<const CT *>(P.K);
     const int np = (P.dbg & 1) ? 0 : kp_high_pair_count(g, P.T.tabs, h);  // wave-uniform
@@ -139,9 +155,9 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         }
     }
     {
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(P.T.tabs);
-        uint32_t *dst = reinterpret_cast<uint32_t *>(lowtabs);
-        const uint32_t words = (uint32_t)g.t * (uint32_t)(sizeof(kp_postab) / 4);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(P.T.pw);
+        uint32_t *dst = reinterpret_cast<uint32_t *>(pw);
+        const uint32_t words = (uint32_t)g.t * 32u;
         for (uint32_t e = threadIdx.x; e < words; e += blockDim.x) dst[e] = src[e];
     }
     // train counts of the block's k-mer-low cells; the level loop aggregates the rest
@@ -188,7 +204,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         sl[NL] = best.y;
         sl[2 * NL] = best.z;
         sl[3 * NL] = best.w;
-        *reinterpret_cast<uint32_t *>(P.C + h * rowstride + lrow) = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+        *reinterpret_cast<uint32_t *>(cd + (size_t)ll * Bpad + 4 * c) = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
     }
     __syncthreads();
 
@@ -207,7 +223,6 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
             if (q < cnt) cur[k] = desc[beg + q];
         }
     }
-    uint8_t *Cb = P.C + h * rowstride + (uint64_t)lane0 * Bpad;
     for (int lam = 0; lam <= lmax; ++lam) {
         const int beg = P.T.loff[lam], cnt = P.T.loff[lam + 1] - beg;
         if (lam < lmax) {
@@ -229,6 +244,9 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                 if (lam == 0) {
                     mt = cm[l];
                     ut = cu[l];
+                } else if (P.dbg & 32) {  // timing ablation: no count recurrence
+                    mt = (CT)l1;
+                    ut = (CT)l2;
                 } else {
                     // count recurrence on the first split (the reference's M_mem/U_mem rows)
                     mt = cm[l1] + cm[l2];
@@ -248,13 +266,22 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                     sc.log1mp = log(1.0 - pr);
                 }
                 uint32_t code[NL];
-                kp_dp_cell_lanes<NL>(g, lowtabs, l, info, st, sc, alpha, beta, pen, code);
+                if (!(P.dbg & 8)) {
+                    kp_dp_cell_lanes<NL>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta, pen,
+                                         code);
+                } else {  // timing ablation: no split scan, keep the single term
+#pragma unroll
+                    for (int j = 0; j < NL; ++j) {
+                        st[l * NL + j] = (float)kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
+                        code[j] = KP_SINGLE;
+                    }
+                }
 #pragma unroll
                 for (int j = 0; j < NL; ++j)
-                    if (code[j] != KP_NONE) Cb[(uint64_t)j * Bpad + l] = (uint8_t)code[j];
+                    if (code[j] != KP_NONE) cd[(size_t)j * Bpad + l] = (uint8_t)code[j];
             }
         }
-        __syncthreads();
+        if (!(P.dbg & 16)) __syncthreads();  // (ablation 16: timing without the level barrier)
 #pragma unroll
         for (int k = 0; k < KP_IPT; ++k) cur[k] = nxt[k];
     }
@@ -265,6 +292,13 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         const float *sl = st + (size_t)(4 * c) * NL + ll;
         *reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c) =
             make_float4(sl[0], sl[NL], sl[2 * NL], sl[3 * NL]);
+    }
+    // ... and its argmin codes, 16 per store
+    const uint32_t nc16 = Bpad / 16;
+    for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nc16; item += blockDim.x) {
+        const uint32_t ll = item / nc16, c = item % nc16;
+        *reinterpret_cast<uint4 *>(P.C + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 16 * c) =
+            *reinterpret_cast<const uint4 *>(cd + (size_t)ll * Bpad + 16 * c);
     }
 }
 
@@ -359,6 +393,7 @@ struct kp_plan {
     uint32_t *d_hlist = nullptr;
     kp_lowdesc *d_ldesc = nullptr;
     uint16_t *d_kl2l = nullptr;
+    uint64_t *d_pw = nullptr;
     // counts
     void *d_K = nullptr;
     int nf = 0;
@@ -389,6 +424,7 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     T.hlist = p->d_hlist;
     T.ldesc = p->d_ldesc;
     T.kl2l = p->d_kl2l;
+    T.pw = p->d_pw;
     return T;
 }
 
@@ -465,7 +501,7 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
         (rc = upload(p, &p->d_lorder, p->hp.lorder)) || (rc = upload(p, &p->d_loff, p->hp.loff)) ||
         (rc = upload(p, &p->d_klofs, p->hp.klofs)) || (rc = upload(p, &p->d_kllist, p->hp.kllist)) ||
         (rc = upload(p, &p->d_hlist, p->hp.hlist)) || (rc = upload(p, &p->d_ldesc, p->hp.ldesc)) ||
-        (rc = upload(p, &p->d_kl2l, p->hp.kl2l))) {
+        (rc = upload(p, &p->d_kl2l, p->hp.kl2l)) || (rc = upload(p, &p->d_pw, p->hp.pw))) {
         kp_plan_destroy(p);
         return rc;
     }
@@ -477,7 +513,7 @@ void kp_plan_destroy(kp_plan *p) {
     if (!p) return;
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
     void *bufs[] = {p->d_tabs, p->d_lowinfo, p->d_lorder, p->d_loff, p->d_klofs, p->d_kllist, p->d_hlist,
-                    p->d_ldesc, p->d_kl2l,
+                    p->d_ldesc, p->d_kl2l, p->d_pw,
                     p->d_K, p->d_S, p->d_C, p->d_groups, p->d_lanegrp, p->d_rtrain, p->d_rtest,
                     p->d_nleaves, p->d_bad, p->d_leaves};
     for (void *b : bufs) dfree(b);
@@ -563,8 +599,8 @@ int kp_set_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers, in
 
 static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
     const kp_geom &g = hp.g;
-    return (size_t)nl * g.Bpad * 4 + 2 * (size_t)g.Bpad * ct_bytes + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) +
-           (size_t)g.t * sizeof(kp_postab) + 16;
+    return (size_t)nl * g.Bpad * 5 + 2 * (size_t)g.Bpad * ct_bytes + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) +
+           (size_t)g.t * 16 * sizeof(uint64_t) + 16;
 }
 
 template <typename CT, int NL>
@@ -595,13 +631,13 @@ static int launch_dp_nl(int nl, kp_ctx *c, const kp_dp_params &P, unsigned nb, u
 
 static int dp_threads() {
     const char *e = getenv("KP_DP_THREADS");
-    int v = e ? atoi(e) : 256;
+    int v = e ? atoi(e) : 512;
     return (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) ? v : 256;
 }
 
 static int lanes_per_wg_default() {
     const char *e = getenv("KP_LANES_PER_WG");
-    int v = e ? atoi(e) : 1;
+    int v = e ? atoi(e) : 3;
     return std::min(std::max(v, 1), KP_GROUP_LANES);
 }
 
@@ -694,6 +730,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.groups = p->d_groups;
     P.lmax = hp.lmax;
     P.dbg = getenv("KP_DEBUG_SKIP") ? atoi(getenv("KP_DEBUG_SKIP")) : 0;
+    P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 0;
     KP_HIP(hipEventRecord(c->ev[0], c->stream));
     uint64_t launches = 0;
     for (int H = 0; H <= hp.hmax; ++H) {

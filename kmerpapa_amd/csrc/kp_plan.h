@@ -39,6 +39,7 @@ struct host_plan {
     int maxlev = 0, hmax = 0, lmax = 0;
     uint64_t n_kmers = 0;
     std::vector<kp_postab> tabs;       // [k]
+    std::vector<uint64_t> pw;          // [t][16] pair words of the low positions (kp_pair_word)
     std::vector<uint32_t> lowinfo;     // [B] packed low digits
     std::vector<uint16_t> lorder;      // [B] low cells sorted by low level
     std::vector<int32_t> loff;         // [lmax + 2]
@@ -109,6 +110,9 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
         g.hcg[i] = g.cgl[t + i] / g.B;
         g.khw[i] = kw[t + i];
     }
+    P.pw.assign((size_t)t * 16, 0);
+    for (int i = 0; i < t; ++i)
+        for (uint32_t d = 0; d < g.r[i]; ++d) P.pw[i * 16 + d] = kp_pair_word(P.tabs[i], d);
     // low cells: digits, levels, order, matching k-mer-low cells
     uint32_t B = g.B;
     if (B > 0xFFFFu) return "block too large for 16-bit cell ids";

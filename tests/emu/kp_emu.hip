@@ -17,7 +17,7 @@
 namespace {
 std::string g_err;
 
-void cell_lanes(int nl, const kp_geom &g, const kp_postab *tabs, uint32_t l, uint32_t info, float *st,
+void cell_lanes(int nl, const kp_geom &g, const uint64_t *tabs, uint32_t l, uint32_t info, float *st,
                 const kp_single_ctx &sc, double a, double b, const double *pen, uint32_t *code) {
     switch (nl) {
         case 1: kp_dp_cell_lanes<1>(g, tabs, l, info, st, sc, a, b, pen, code); break;
@@ -126,7 +126,7 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
                             sc.log1mp = log(1.0 - p);
                         }
                         uint32_t code[KP_GROUP_LANES];
-                        cell_lanes(G.nl, g, hp.tabs.data(), l, D.info, st.data(), sc, G.alpha, G.beta, G.pen, code);
+                        cell_lanes(G.nl, g, hp.pw.data(), l, D.info, st.data(), sc, G.alpha, G.beta, G.pen, code);
                         for (int j = 0; j < G.nl; ++j)
                             if (code[j] != KP_NONE) C[kp_lane_row(g, h, (uint32_t)G.lane0 + j) + l] = (uint8_t)code[j];
                     }
