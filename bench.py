@@ -111,18 +111,28 @@ def cpu_baseline(prep, seconds_hint=15.0):
                       f"({O.npat(sub)} cells x {NFOLDS} folds, 1 (alpha,c)) in {dt:.1f} s on 1 host core"}
 
 
-def committed_traffic(gen_pat, n_lanes):
-    """HBM bytes per DP pass measured with rocprofv3 PMC counters (profiles/pmc_*.json)."""
+def committed_traffic(gen_pat, n_lanes, kernel_tag):
+    """HBM bytes per DP pass measured with rocprofv3 PMC counters: the newest
+    profiles/<round>/pmc_*.json (tools/pmc_json.py) taken with the same kernel build."""
+    import glob
     best = None
-    for name in sorted(os.listdir(os.path.join(ROOT, "profiles"))) if os.path.isdir(os.path.join(ROOT, "profiles")) else []:
-        if name.startswith("pmc_") and name.endswith(".json"):
-            try:
-                d = json.load(open(os.path.join(ROOT, "profiles", name)))
-            except ValueError:
-                continue
-            if d.get("gen_pat") == gen_pat and d.get("lanes") == n_lanes:
-                best = d
+    for fn in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "pmc_*.json"))):
+        try:
+            d = json.load(open(fn))
+        except ValueError:
+            continue
+        if d.get("gen_pat") == gen_pat and d.get("lanes") == n_lanes and d.get("kernel_tag") == kernel_tag:
+            best = dict(d, source=os.path.relpath(fn, ROOT))
     return best
+
+
+def full_cv(plan, prep, rank, world):
+    """The whole 5x5 grid x 5 folds as the CV driver runs it: this rank's share of the
+    (alpha, fold) groups, one pass each, root read-out included."""
+    t0 = time.perf_counter()
+    mine = prep["groups"][rank::world]
+    roots = [plan.run([g]) for g in mine]
+    return time.perf_counter() - t0, len(mine), roots
 
 
 def main():
@@ -133,6 +143,7 @@ def main():
     ap.add_argument("--pattern", default=GEN_PAT)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--max-block", type=int, default=0)
+    ap.add_argument("--no-full-cv", action="store_true", help="skip the full 5x5x5 CV wall-clock leg")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -182,7 +193,21 @@ def main():
     alg = sum(s["alg_bytes"] for s in stats)
     achieved = alg / (dp_ms / 1e3) / 1e9
     lanes = len(groups[0][3])
-    tr = committed_traffic(gen_pat, lanes)
+    tag = engine.kernel_tag()
+    tr = committed_traffic(gen_pat, lanes, tag)
+
+    # 9-mer 5-fold CV wall-clock (BASELINE.json's second metric): fold split (host, every
+    # rank) + this rank's passes, max over ranks
+    cv_wall = None
+    if not a.no_full_cv:
+        barrier()
+        t_cv, n_mine, _ = full_cv(plan, prep, rank, world)
+        cv_wall = prep["t_fold_s"] + t_setup + t_cv
+        if dist is not None:
+            import torch
+            t = torch.tensor([cv_wall], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            cv_wall = float(t.item())
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
         passes_full_cv = math.ceil(len(groups) / world)
@@ -207,15 +232,26 @@ def main():
                        "alphas": ALPHAS, "penalties": PENALTIES, "nfolds": NFOLDS},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": (tr["hbm_bytes_per_pass"] if tr else None)},
+                         "traffic": (tr["hbm_bytes_per_pass"] if tr else None),
+                         "kernel": "kp_dp_kernel (all launches of one pass)",
+                         "alg_bytes_per_pass": alg / a.steps,
+                         "alg_bytes_per_unit": alg / units_rank,
+                         "basis": "SURVEY.md 8(d) per-unit algorithmic bytes x units / HIP-event time of the "
+                                  "pass's kp_dp_kernel launches; traffic = PMC HBM bytes per pass"},
             "dp_kernel_ms_per_step": dp_ms / a.steps,
+            "dp_kernel_launches_per_step": sum(s["dp_launches"] for s in stats) / a.steps,
+            "dp_kernel_avg_launch_ms": dp_ms / max(1, sum(s["dp_launches"] for s in stats)),
             "backtrack_ms_per_step": sum(s["backtrack_ms"] for s in stats) / a.steps,
-            "cv_5x5x5_wall_s": passes_full_cv * ms_step / 1e3,
+            "cv_5x5x5_wall_s": cv_wall,
+            "cv_5x5x5_wall_s_estimate": prep["t_fold_s"] + t_setup + passes_full_cv * ms_step / 1e3,
             "fold_split_s": prep["t_fold_s"],
             "setup_s": t_setup,
+            "kernel_tag": tag,
         }
         if tr:
             line["roofline"]["traffic_source"] = tr.get("source")
+            line["roofline"]["traffic_gbs"] = tr["hbm_bytes_per_pass"] / (dp_ms / a.steps / 1e3) / 1e9
+            line["roofline"]["traffic_frac"] = line["roofline"]["traffic_gbs"] / PEAK_HBM_GBS
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(prep)
         else:

@@ -103,6 +103,18 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+def kernel_tag():
+    """Short hash of the HIP sources the library was built from (ties profiles to a build)."""
+    import hashlib
+    h = hashlib.sha1()
+    src = os.path.join(_HERE, "csrc")
+    for name in sorted(os.listdir(src)):
+        if name.endswith((".hip", ".h")):
+            with open(os.path.join(src, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:12]
+
+
 def device_count():
     n = ctypes.c_int(0)
     _check(load().kp_device_count(ctypes.byref(n)))

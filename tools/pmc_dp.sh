@@ -9,7 +9,7 @@ R=$GRAFT_REPO_ROOT
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$R/$out/$name" -o run -- \
-    python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline > "$R/$out/$name.log" 2>&1
+    python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-full-cv > "$R/$out/$name.log" 2>&1
   echo "pass $name rc=$?"
 }
 run sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS

@@ -1,0 +1,37 @@
+"""Turn rocprofv3 FETCH_SIZE / WRITE_SIZE passes over one bench step into the per-pass HBM
+traffic record bench.py reports as roofline.traffic.
+
+usage: python tools/pmc_json.py <pmc dir with fetch/ and write/ passes> <out.json> [lanes]
+gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half the bytes of 16-B/lane
+streaming reads -> x2; WRITE_SIZE is exact for 16-B/lane stores.  Units are KB (x1024).
+"""
+import csv, glob, json, os, sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from kmerpapa_amd import engine  # noqa: E402
+
+d, out = sys.argv[1], sys.argv[2]
+lanes = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+
+
+def total(pass_name, counter):
+    s, n = 0.0, 0
+    for fn in glob.glob(os.path.join(d, pass_name, "*counter_collection.csv")):
+        for r in csv.DictReader(open(fn)):
+            if "kp_dp_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                s += float(r["Counter_Value"])
+                n += 1
+    return s, n
+
+
+fetch, nf = total("fetch", "FETCH_SIZE")
+write, nw = total("write", "WRITE_SIZE")
+rec = {"gen_pat": "NNNNMNNNN", "lanes": lanes, "kernel_tag": engine.kernel_tag(),
+       "dp_launches": nf, "fetch_size_kb": fetch, "write_size_kb": write,
+       "hbm_read_bytes_per_pass": 2 * fetch * 1024, "hbm_write_bytes_per_pass": write * 1024,
+       "hbm_bytes_per_pass": 2 * fetch * 1024 + write * 1024,
+       "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
+                 "`bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-full-cv`, kp_dp_kernel dispatches "
+                 "summed; FETCH_SIZE x2 (gfx950 16-B/lane read correction), KB x1024"}
+json.dump(rec, open(out, "w"), indent=1)
+print(json.dumps(rec))
