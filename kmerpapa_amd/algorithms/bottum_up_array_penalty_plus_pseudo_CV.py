@@ -116,6 +116,23 @@ def _f64_sum(values):
     return acc
 
 
+def _distributed_runner():
+    """Under torch.distributed (one process per GPU, e.g. torchrun), each rank runs its
+    chunk of the groups on GPU LOCAL_RANK and the root scalars are all-gathered
+    (kmerpapa_amd.shard); otherwise every visible GPU of this process is used."""
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            import os
+            from ..shard import sharded_run_groups, torch_all_gather
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            return sharded_run_groups(engine.run_groups, dist.get_rank(), dist.get_world_size(),
+                                      torch_all_gather(), devices=[local]), [local]
+    except ImportError:
+        pass
+    return engine.run_groups, engine.visible_devices()
+
+
 def pattern_partition_bottom_up(gen_pat, contextD, alphas, args, nmut, nunmut, penalties, index_mut=0):
     """Grid CV over (alpha, penalty); returns ``(best_alpha, best_penalty, best_test_loss)`` (CV :81-177)."""
     nf = args.nfolds
@@ -124,8 +141,9 @@ def pattern_partition_bottom_up(gen_pat, contextD, alphas, args, nmut, nunmut, p
     itype = _itype(nmut, nunmut)
     if index_mut != 0:
         contextD = {k: (v[index_mut], v[-1]) for k, v in contextD.items()}
+    run_groups, devices = _distributed_runner()
     res = cv_roots(gen_pat, contextD, list(alphas), list(penalties), nf, args.seed, nit, itype,
-                   devices=engine.visible_devices(), verbose=verbosity)
+                   devices=devices, verbose=verbosity, run_groups=run_groups)
     best_test_loss = 1e100
     best_values = (None, None)
     for a_i, alpha in enumerate(alphas):

@@ -345,17 +345,8 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     devices = list(devices) if devices is not None else visible_devices()[:1]
     if not devices:
         raise KPError(-3, "no GPU visible")
-    lane_counts = [len(g[3]) for g in groups]
-    total = sum(lane_counts)
-    # contiguous chunks of roughly equal lanes
-    bounds, acc, d = [0], 0, 0
-    for i, n in enumerate(lane_counts):
-        acc += n
-        if d < len(devices) - 1 and acc >= total * (d + 1) / len(devices):
-            bounds.append(i + 1)
-            d += 1
-    while len(bounds) < len(devices) + 1:
-        bounds.append(len(groups))
+    from .shard import chunk_bounds
+    bounds = chunk_bounds([len(g[3]) for g in groups], len(devices))  # contiguous, lane-balanced
     results = [None] * len(devices)
     errors = []
 

@@ -1,0 +1,85 @@
+"""Multi-rank sharding of the CV grid (kmerpapa_amd.shard), world_size 2 over gloo on the
+CPU, with the host emulator of the blocked DP standing in for the GPU: the sharded CV
+driver must return exactly the single-process roots, every group run exactly once."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from kmerpapa_amd import shard
+from tests.fixtures import golden_json
+
+
+def test_chunk_bounds_cover_every_group_once():
+    for n in range(0, 30):
+        lanes = [1 + (i * 7) % 5 for i in range(n)]
+        for parts in (1, 2, 3, 4, 8):
+            b = shard.chunk_bounds(lanes, parts)
+            assert len(b) == parts + 1 and b[0] == 0 and b[-1] == n
+            assert all(b[i] <= b[i + 1] for i in range(parts))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _work(rank, world, q)
+    except Exception as e:  # reported to the parent instead of hanging it
+        q.put((rank, None, repr(e), []))
+    finally:
+        dist.destroy_process_group()
+
+
+def _work(rank, world, q):
+    if True:
+        from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+        from tests.emu import emu as E
+        c = golden_json("small_dp.json")["cases"]["k3"]
+        ctx = {k: tuple(v) for k, v in c["contextD"].items()}
+        ran = []
+
+        def counting(gen_pat, M, U, groups, devices=None, max_block=0):
+            ran.extend((g[0], g[1], tuple(g[3])) for g in groups)
+            return E.run_groups(gen_pat, M, U, groups, devices=devices, max_block=max_block)
+        run = shard.sharded_run_groups(counting, rank, world, shard.torch_all_gather())
+        res = cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], 1, np.uint32,
+                           run_groups=run)
+        q.put((rank, res["train"].tobytes(), res["test"].tobytes(), ran))
+
+
+def test_two_rank_gloo_cv_matches_single_process():
+    import multiprocessing as mp
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    from tests.emu import emu as E
+    c = golden_json("small_dp.json")["cases"]["k3"]
+    ctx = {k: tuple(v) for k, v in c["contextD"].items()}
+    ref = cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], 1, np.uint32,
+                       run_groups=E.run_groups)
+    ctxm = mp.get_context("spawn")
+    q = ctxm.Queue()
+    port = _free_port()
+    procs = [ctxm.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    outs = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ran_all = []
+    for rank, tr, te, ran in outs:
+        assert tr is not None, f"rank {rank} failed: {te}"
+        assert tr == ref["train"].tobytes() and te == ref["test"].tobytes(), f"rank {rank} roots differ"
+        ran_all.extend(ran)
+    want = [(f, a, tuple(c["penalties"])) for a in c["alphas"] for f in range(c["nfolds"])]
+    assert sorted(ran_all) == sorted(want)  # every (alpha, fold) group exactly once over both ranks
+    assert all(len(r) > 0 for _, _, _, r in outs)  # both ranks did work
