@@ -223,16 +223,21 @@ __host__ __device__ inline uint64_t kp_pair_word(const kp_postab &T, uint32_t d)
     return w;
 }
 
-// first-min over NP split pairs of one position for NL lanes; all 2*NP*NL LDS reads are
-// issued before the first compare (fully unrolled, no loop-carried dependence on loads)
 // 24-bit multiply (operands known < 2^24: one full-rate v_mul_u32_u24 on gfx950)
 __host__ __device__ inline uint32_t kp_mul24(uint32_t a, uint32_t b) { return (a & 0xFFFFFFu) * (b & 0xFFFFFFu); }
 
-// SP = pointer to the block's scores: float* on the host, an LDS (address space 3) pointer
-// in the kernels so every address is 32-bit
+// ---------------------------------------------------------------------------
+// VALUE-ONLY DP.  A cell's stored float32 score is min(best split, single term) and does
+// not depend on which candidate achieved it, so the sweep keeps values only and the
+// argmin (with the reference's first-wins tie rule) is recomputed for the few cells of
+// the optimal tree at backtrack time (kp_cell_decide).  Split candidates combine with
+// fminf: it ignores NaN exactly as "v < best" does, and every score is >= +0 (no -0).
+// ---------------------------------------------------------------------------
+
+// min over NP split pairs of one low position, NL lanes; all 2*NP*NL LDS reads issue
+// before the first min (fully unrolled)
 template <int NL, int NP, typename SP>
-__host__ __device__ inline void kp_pairs_min(SP st, uint32_t l, uint32_t cg, uint64_t w, uint32_t code0,
-                                             float *lbest, uint32_t *lcode) {
+__host__ __device__ inline void kp_pairs_minv(SP st, uint32_t l, uint32_t cg, uint64_t w, float *lmin) {
     float va[NP][NL], vb[NP][NL];
     const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
 #pragma unroll
@@ -247,129 +252,231 @@ __host__ __device__ inline void kp_pairs_min(SP st, uint32_t l, uint32_t cg, uin
         }
     }
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
+    for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            const float v = va[p][j] + vb[p][j];
-            if (v < lbest[j]) {
-                lbest[j] = v;
-                lcode[j] = code0 | (uint32_t)p;
-            }
-        }
-    }
+        for (int j = 0; j < NL; ++j) lmin[j] = fminf(lmin[j], va[p][j] + vb[p][j]);
 }
 
-// ---------------------------------------------------------------------------
-// one DP cell for NL lanes at once (lanes interleaved in LDS: st[cell * NL + lane]).
-// pw = pair words [t][16] (kp_pair_word).  code_out[lane] = KP_NONE when the gathered
-// high-position winner stands (its code is already stored), else the new argmin code.
-// ---------------------------------------------------------------------------
+
+// one DP cell for NL lanes (lanes interleaved in LDS: st[cell * NL + lane]); st[l] holds
+// the best high-position split gathered from HBM.  pw = pair words [t][16].
 template <int NL, typename SP, typename WP>
-__host__ __device__ inline void kp_dp_cell_lanes(const kp_geom &g, WP pw, uint32_t l, uint32_t lowinfo, SP st,
-                                                 const kp_single_ctx &sc, double alpha, double beta, const double *pen,
-                                                 uint32_t *code_out) {
+__host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint32_t l, uint32_t lowinfo, SP st,
+                                                  const kp_single_ctx &sc, double alpha, double beta,
+                                                  const double *pen) {
     SP row = st + l * NL;
     if (sc.kmer) {  // level 0 (CV :145-151 / Fit :106-114)
 #pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
-            code_out[j] = KP_SINGLE;
-        }
+        for (int j = 0; j < NL; ++j) row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
         return;
     }
-    float lbest[NL];
-    uint32_t lcode[NL];
+    float lmin[NL];
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
-        lbest[j] = __builtin_huge_valf();
-        lcode[j] = KP_NONE;
-    }
-    // one pair word per low position, all loaded up front
+    for (int j = 0; j < NL; ++j) lmin[j] = row[j];
     uint64_t w[KP_MAXT];
 #pragma unroll
     for (int i = 0; i < KP_MAXT; ++i) w[i] = (i < g.t) ? pw[i * 16 + kp_low_digit(lowinfo, i)] : 0;
-    // positions in scan order; np is 0, 1, 3 or 7 for every IUPAC code and, because cells
-    // of a wave share their split signature (kp_plan.h), nearly always wave-uniform
+    // np is 0, 1, 3 or 7 for every IUPAC code and, because cells of a wave share their
+    // split signature (kp_plan.h), nearly always wave-uniform
 #pragma unroll
     for (int i = 0; i < KP_MAXT; ++i) {
         if (i >= g.t) continue;
         const uint32_t np = (uint32_t)(w[i] >> 56);
         const uint32_t cg = (uint32_t)g.cgl[i] & 0xFFFFu;  // low place values are < 2^16 (block <= 65535)
-        const uint32_t code0 = (uint32_t)i << 3;
         if (np == 1) {
-            kp_pairs_min<NL, 1>(st, l, cg, w[i], code0, lbest, lcode);
+            kp_pairs_minv<NL, 1>(st, l, cg, w[i], lmin);
         } else if (np == 3) {
-            kp_pairs_min<NL, 3>(st, l, cg, w[i], code0, lbest, lcode);
+            kp_pairs_minv<NL, 3>(st, l, cg, w[i], lmin);
         } else if (np == 7) {
-            kp_pairs_min<NL, 7>(st, l, cg, w[i], code0, lbest, lcode);
+            kp_pairs_minv<NL, 7>(st, l, cg, w[i], lmin);
         } else {
             for (uint32_t p = 0; p < np; ++p) {  // not produced by the IUPAC tables; kept general
                 const uint32_t l1 = l - (uint32_t)((w[i] >> (8 * p)) & 15u) * cg;
                 const uint32_t l2 = l - (uint32_t)((w[i] >> (8 * p + 4)) & 15u) * cg;
 #pragma unroll
-                for (int j = 0; j < NL; ++j) {
-                    const float v = st[l1 * NL + j] + st[l2 * NL + j];
-                    if (v < lbest[j]) {
-                        lbest[j] = v;
-                        lcode[j] = code0 | p;
-                    }
-                }
+                for (int j = 0; j < NL; ++j) lmin[j] = fminf(lmin[j], st[l1 * NL + j] + st[l2 * NL + j]);
             }
         }
     }
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-        float best = row[j];
-        uint32_t code = KP_NONE;
-        if (lcode[j] != KP_NONE && !(best < lbest[j])) {  // low positions precede high ones in scan order
-            best = lbest[j];
-            code = lcode[j];
-        }
+        float best = lmin[j];
         const double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
-        if (s < (double)best) {
-            best = (float)s;
-            code = KP_SINGLE;
-        }
+        if (s < (double)best) best = (float)s;  // float64 compare against the float32 store (CV :71)
         row[j] = best;
-        code_out[j] = code;
     }
 }
 
 // ---------------------------------------------------------------------------
-// backtrack of one lane: DFS over the argmin tree from the root.
-// Returns the test -2LL of the root (CV :159-163) computed with the reference's f32
-// sums test[c1] + test[c2]; optionally lists leaves in reference order (Fit :17-24).
+// separable count tables of one block (train counts of one group fold).
+// T_0[kl] = the block's k-mer-low rows; T_{s+1} expands low position s from nucleotides
+// to digits (sum over the digit's nucleotides); T_{t-1} = ptab.  Cell l's counts are then
+// a sum of <= 4 ptab entries (kp_ptab_counts).  lm = nucleotide masks [t][16].
+// Entries are (M, U) pairs of CT.  tid/nth = this thread and the thread count; sync()
+// separates the steps (a workgroup barrier on the GPU, nothing on the host).
 // ---------------------------------------------------------------------------
+template <typename CT, typename LM, typename SyncFn>
+__host__ __device__ inline void kp_build_count_table(const kp_geom &g, const CT *K, uint64_t h, int fold, LM lm,
+                                                     CT *bufA, CT *bufB, CT *ptab, uint32_t tid, uint32_t nth,
+                                                     SyncFn sync) {
+    CT *out0 = (g.t == 1) ? ptab : bufA;
+    for (uint32_t kl = tid; kl < g.n_kl; kl += nth) {
+        const kp_cnt c = kp_kl_counts<CT>(g, K, h, kl, fold);
+        out0[2 * kl] = (CT)c.mtr;
+        out0[2 * kl + 1] = (CT)c.utr;
+    }
+    CT *in = out0;
+    uint32_t Rs = 1;
+    for (int s = 0; s + 1 < g.t; ++s) {
+        sync();
+        uint32_t rest = 1;
+        for (int i = s + 1; i < g.t; ++i) rest *= g.n[i];
+        const uint32_t rs = g.r[s], ns = g.n[s];
+        const uint32_t entries = Rs * rs * rest;
+        CT *out = (s + 2 == g.t) ? ptab : (in == bufA ? bufB : bufA);
+        for (uint32_t e = tid; e < entries; e += nth) {
+            const uint32_t D = e % Rs, q = e / Rs, ds = q % rs, Nr = q / rs;
+            const uint32_t m = lm[s * 16 + ds];
+            CT sm = 0, su = 0;
+            for (uint32_t a = 0; a < ns; ++a)
+                if (m & (1u << a)) {
+                    const uint32_t src = D + Rs * (a + ns * Nr);
+                    sm += in[2 * src];
+                    su += in[2 * src + 1];
+                }
+            out[2 * e] = sm;
+            out[2 * e + 1] = su;
+        }
+        in = out;
+        Rs *= rs;
+    }
+}
+
+// train counts of low cell l (packed low digits info) from the block's count table
+template <typename CT, typename LM, typename PT>
+__host__ __device__ inline void kp_ptab_counts(const kp_geom &g, LM lm, PT ptab, uint32_t l, uint32_t info,
+                                               uint64_t *mtr, uint64_t *utr) {
+    const int tl = g.t - 1;
+    const uint32_t Rl = (uint32_t)g.cgl[tl];
+    const uint32_t dl = kp_low_digit(info, tl);
+    const uint32_t m = lm[tl * 16 + dl];
+    const uint32_t base = l - dl * Rl;
+    CT mt = 0, ut = 0;
+    for (uint32_t c = 0; c < g.n[tl]; ++c)
+        if (m & (1u << c)) {
+            mt += ptab[2 * (base + Rl * c)];
+            ut += ptab[2 * (base + Rl * c) + 1];
+        }
+    *mtr = (uint64_t)mt;
+    *utr = (uint64_t)ut;
+}
+
+// ---------------------------------------------------------------------------
+// whole-lattice helpers for the backtrack (cells addressed by their global index)
+// ---------------------------------------------------------------------------
+
+// packed digits of cell x, 4 bits per position
+__host__ __device__ inline uint64_t kp_cell_digits(const kp_geom &g, uint64_t x) {
+    uint64_t w = 0;
+    for (int i = 0; i < g.k; ++i) {
+        w |= (x % g.r[i]) << (4 * i);
+        x /= g.r[i];
+    }
+    return w;
+}
+
+__host__ __device__ inline uint32_t kp_dig(uint64_t dig, int i) { return (uint32_t)(dig >> (4 * i)) & 15u; }
+
+__host__ __device__ inline bool kp_dig_is_kmer(const kp_geom &g, uint64_t dig) {
+    for (int i = 0; i < g.k; ++i)
+        if (kp_dig(dig, i) >= g.n[i]) return false;
+    return true;
+}
+
+// train/test counts of cell x for a group fold: K rows of its block over the matching
+// k-mer-low cells (sums are exact in itype, so any order equals the reference's)
 template <typename CT>
-__host__ __device__ inline float kp_leaf_test(const kp_geom &g, const kp_postab *tabs, const uint32_t *lowinfo_tab,
-                                              const uint32_t *klofs, const uint16_t *kllist, const CT *K,
-                                              uint64_t x, int fold, double alpha, double beta) {
-    uint64_t h = x / g.B;
-    uint32_t l = (uint32_t)(x % g.B);
+__host__ __device__ inline kp_cnt kp_cell_counts(const kp_geom &g, const uint32_t *klofs, const uint16_t *kllist,
+                                                 const CT *K, uint64_t x, int fold) {
+    const uint64_t h = x / g.B;
+    const uint32_t l = (uint32_t)(x % g.B);
     kp_cnt c = {0, 0, 0, 0};
     for (uint32_t q = klofs[l]; q < klofs[l + 1]; ++q) {
-        kp_cnt e = kp_kl_counts<CT>(g, K, h, kllist[q], fold);
-        c.mtr += e.mtr; c.utr += e.utr; c.mte += e.mte; c.ute += e.ute;
+        const kp_cnt e = kp_kl_counts<CT>(g, K, h, kllist[q], fold);
+        c.mtr += e.mtr;
+        c.utr += e.utr;
+        c.mte += e.mte;
+        c.ute += e.ute;
     }
+    return c;
+}
+
+// test -2LL term of a leaf (CV :73-78; level 0: score_test_folds :15-20)
+__host__ __device__ inline float kp_leaf_test_term(const kp_cnt &c, bool kmer, int fold, double alpha, double beta) {
     if (fold < 0) return 0.0f;
-    if (kp_is_kmer(g, h, lowinfo_tab[l])) return kp_kmer_test(c, alpha, beta);
-    double p = kp_rate(c, alpha, beta);
+    if (kmer) return kp_kmer_test(c, alpha, beta);
+    const double p = kp_rate(c, alpha, beta);
     return kp_single_test(c, log(p), log(1.0 - p));
 }
 
+// The reference's decision for one cell, recomputed from final child scores: splits in
+// scan order (positions ascending, pairs in table order, strict "<" from +inf), then the
+// single term in float64 (CV :36-78, Fit :37-64).  SF(cell) -> float32 score.  Returns the
+// code ((pos << 3) | pair, or KP_SINGLE) and the cell's value in *value.
+template <typename SF>
+__host__ __device__ inline uint32_t kp_cell_decide(const kp_geom &g, const kp_postab *tabs, uint64_t x, uint64_t dig,
+                                                   SF score, const kp_cnt &c, double alpha, double beta, double pen,
+                                                   float *value) {
+    if (kp_dig_is_kmer(g, dig)) {
+        *value = kp_kmer_train(c, alpha, beta, pen);
+        return KP_SINGLE;
+    }
+    float best = __builtin_huge_valf();
+    uint32_t code = KP_NONE;
+    for (int i = 0; i < g.k; ++i) {
+        const uint32_t d = kp_dig(dig, i);
+        const kp_postab &T = tabs[i];
+        for (int j = 0; j < T.np[d]; ++j) {
+            const uint64_t c1 = x - (uint64_t)(d - T.pa[d][j]) * g.cgl[i];
+            const uint64_t c2 = x - (uint64_t)(d - T.pb[d][j]) * g.cgl[i];
+            const float v = score(c1) + score(c2);
+            if (v < best) {
+                best = v;
+                code = (uint32_t)((i << 3) | j);
+            }
+        }
+    }
+    const double p = kp_rate(c, alpha, beta);
+    const double s = kp_single_train(c, log(p), log(1.0 - p), pen);
+    if (s < (double)best) {
+        best = (float)s;
+        code = KP_SINGLE;
+    }
+    *value = best;
+    return code;
+}
+
+// ---------------------------------------------------------------------------
+// sequential backtrack of one lane (host emulator; the GPU runs a breadth-first version):
+// DFS over the recomputed argmin tree from the root.  Returns the root's test -2LL summed
+// along the tree in float32 (test[c1] + test[c2], CV :47) and lists the leaves in the
+// reference's order (left subtree first, Fit :17-24).
+//   decide(x, dig, &cnt) -> code   leaf(x, dig, cnt) -> test term
+// ---------------------------------------------------------------------------
 struct kp_frame {
-    uint64_t x, x2;
+    uint64_t x, dig, x2, dig2;
     float v1;
     uint32_t st;
 };
 
-template <typename LeafFn>
-__host__ __device__ inline float kp_backtrack_lane(const kp_geom &g, const kp_postab *tabs, const uint8_t *C,
-                                                   uint32_t lane, LeafFn leaf, uint64_t *leaves, uint64_t cap,
-                                                   uint64_t *nleaves, uint32_t *bad) {
+template <typename DecideFn, typename LeafFn>
+__host__ __device__ inline float kp_backtrack_dfs(const kp_geom &g, const kp_postab *tabs, DecideFn decide,
+                                                  LeafFn leaf, uint64_t *leaves, uint64_t cap, uint64_t *nleaves,
+                                                  uint32_t *bad) {
     kp_frame stk[KP_MAXDEPTH];
     int sp = 1;
     stk[0].x = g.nblocks * g.B - 1;  // the general pattern is the last cell
+    stk[0].dig = kp_cell_digits(g, stk[0].x);
     stk[0].st = 0;
     float ret = 0.0f;
     uint64_t nl = 0;
@@ -377,24 +484,27 @@ __host__ __device__ inline float kp_backtrack_lane(const kp_geom &g, const kp_po
     while (sp > 0) {
         kp_frame &f = stk[sp - 1];
         if (f.st == 0) {
-            uint64_t h = f.x / g.B;
-            uint32_t l = (uint32_t)(f.x % g.B);
-            uint32_t code = C[kp_lane_row(g, h, lane) + l];
+            kp_cnt c;
+            const uint32_t code = decide(f.x, f.dig, &c);
             if (code == KP_SINGLE || code == KP_NONE) {
                 if (code == KP_NONE) err = 1;
-                ret = leaf(f.x);
+                ret = leaf(f.x, f.dig, c);
                 if (leaves && nl < cap) leaves[nl] = f.x;
                 ++nl;
                 --sp;
             } else {
-                int i = (int)(code >> 3), j = (int)(code & 7u);
-                uint32_t d = (uint32_t)((f.x / g.cgl[i]) % g.r[i]);
+                const int i = (int)(code >> 3), j = (int)(code & 7u);
+                const uint32_t d = kp_dig(f.dig, i);
                 const kp_postab &T = tabs[i];
-                uint64_t x1 = f.x - (uint64_t)(d - T.pa[d][j]) * g.cgl[i];
+                const uint64_t clear = ~(15ull << (4 * i));
+                const uint64_t x1 = f.x - (uint64_t)(d - T.pa[d][j]) * g.cgl[i];
+                const uint64_t dig1 = (f.dig & clear) | ((uint64_t)T.pa[d][j] << (4 * i));
                 f.x2 = f.x - (uint64_t)(d - T.pb[d][j]) * g.cgl[i];
+                f.dig2 = (f.dig & clear) | ((uint64_t)T.pb[d][j] << (4 * i));
                 f.st = 1;
                 if (sp >= KP_MAXDEPTH) { err = 2; break; }
                 stk[sp].x = x1;
+                stk[sp].dig = dig1;
                 stk[sp].st = 0;
                 ++sp;
                 continue;
@@ -404,6 +514,7 @@ __host__ __device__ inline float kp_backtrack_lane(const kp_geom &g, const kp_po
             f.st = 2;
             if (sp >= KP_MAXDEPTH) { err = 2; break; }
             stk[sp].x = f.x2;
+            stk[sp].dig = f.dig2;
             stk[sp].st = 0;
             ++sp;
             continue;

@@ -1,18 +1,28 @@
 // kp_hip.hip -- gfx950 kernels and C-ABI of the blocked lattice DP (libkmerpapa_hip.so).
 //
-// Kernels (one launch per high level for the first two, kp_core.h for the layout):
-//   kp_counts_kernel    : per-block k-mer-low fold counts K[h] (replaces the first-pair
-//                         M/U aggregation, CV :52-55, Fit :50-53)
-//   kp_dp_kernel        : the DP of every cell of one block for one lane group
-//                         (CV handle_pattern :26-78 / score_test_folds :15-20,
-//                          Fit handle_pattern :31-64 / score :26-29)
-//       phase 1  gather: every high-position split pair = two coalesced float4 reads of
-//                        whole child-block rows (HBM/L2), first-min in scan order
-//       phase 2  levels: low-position splits inside LDS, level by level, then the
-//                        single-pattern term in float64
-//       phase 3  store : train row (f32) + argmin codes (u8), coalesced
-//   kp_backtrack_kernel : root read-out; test -2LL of the root by a DFS over the argmin
-//                         tree (CV :158-163), leaves for the Fit (Fit :17-24)
+// The sweep is VALUE-ONLY (kp_core.h): a cell's float32 score does not depend on which
+// candidate won, so only scores are stored; the argmin of the few cells on the optimal
+// tree is recomputed with the reference's tie rule at backtrack time.
+//
+// Kernels:
+//   kp_counts_kernel : per-block fold counts K[h] of the block's k-mer-low cells (replaces
+//                      the first-pair M/U aggregation, CV :52-55, Fit :50-53); one launch
+//                      per high level, once per fold table
+//   kp_dp_kernel     : the DP of every cell of one block for NL lanes (CV handle_pattern
+//                      :26-78 / score_test_folds :15-20, Fit handle_pattern :31-64 / score
+//                      :26-29); one launch per (high level, lane class)
+//       counts : separable count tables of the block in LDS (no recurrence)
+//       gather : every high-position split pair = two coalesced float4 reads of whole
+//                child-block rows (HBM/L2), min-reduced
+//       levels : low-position splits inside LDS, level by level, then the float64
+//                single-pattern term
+//       store  : the block's score rows, float4
+//   kp_bt_*          : breadth-first backtrack of every lane at once: one wave per tree
+//                      node recomputes the node's decision (kp_cell_decide semantics),
+//                      checks it reproduces the stored score, and appends the children;
+//                      kp_bt_finish sums the test -2LL along the tree in float32 (CV
+//                      :158-163) and lists the leaves in the reference's order (Fit :17-24)
+//   kp_codes_kernel  : argmin code of every cell (parity dumps only)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -41,14 +51,14 @@ typedef __attribute__((address_space(3))) uint64_t kp_lds_u64;
 struct kp_dev_tables {
     const kp_postab *tabs;
     const uint32_t *lowinfo;
-    const uint16_t *lorder;
     const int32_t *loff;
     const uint32_t *klofs;
     const uint16_t *kllist;
     const uint32_t *hlist;
     const kp_lowdesc *ldesc;
-    const uint16_t *kl2l;
     const uint64_t *pw;
+    const uint64_t *hdig;
+    const uint8_t *lowmask;
 };
 
 template <typename CT>
@@ -92,36 +102,54 @@ struct kp_dp_params {
     kp_dev_tables T;
     const void *K;
     float *S;
-    uint8_t *C;
     const kp_group_dev *groups;
     uint64_t hbase;
     int H;
     int lmax;
+    uint32_t ptab_entries;     // separable count table entries (kp_plan.h)
+    uint32_t pscratch_entries; // largest intermediate table of its build
     int remap;  // 1 = XCD-contiguous block order (KP_XCD_REMAP=1; measured 4% slower, off by default)
+    unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
     int dbg;  // timing ablation only (KP_DEBUG_SKIP, wrong results): 1 = skip gather, 2 = skip level phase,
-              // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier, 32 = no count recurrence
+              // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier
 };
 
-// first-min update of one float4 of candidates (strict "<": the earlier pair keeps ties)
-__device__ inline void kp_min4(float4 &best, uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3, const float4 a,
-                               const float4 b, uint32_t code) {
-    float v;
-    v = a.x + b.x; if (v < best.x) { best.x = v; c0 = code; }
-    v = a.y + b.y; if (v < best.y) { best.y = v; c1 = code; }
-    v = a.z + b.z; if (v < best.z) { best.z = v; c2 = code; }
-    v = a.w + b.w; if (v < best.w) { best.w = v; c3 = code; }
-}
+#ifdef KP_STAMPS
+// diagnostic build: lane 0 of every workgroup sums the shader-clock ticks of each phase
+// in LDS and flushes them with one global atomic per slot at the end (never read by the
+// kernel; outputs are unchanged)
+#define KP_STAMP(slot)                                                                        \
+    do {                                                                                      \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                           \
+        if (threadIdx.x == 0) st_lds[slot] += t_ - st_prev;                                   \
+        st_prev = t_;                                                                         \
+    } while (0)
+#else
+#define KP_STAMP(slot) \
+    do {               \
+    } while (0)
+#endif
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
+
+// float4 min-update with a split candidate a + b (fminf drops NaN candidates like "<")
+__device__ inline void kp_min4v(float4 &best, const float4 a, const float4 b) {
+    best.x = fminf(best.x, a.x + b.x);
+    best.y = fminf(best.y, a.y + b.y);
+    best.z = fminf(best.z, a.z + b.z);
+    best.w = fminf(best.w, a.w + b.w);
+}
 
 template <typename CT, int NL>
 __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const kp_geom &g = P.g;
-    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so give each XCD a
-    // contiguous run of the level's block list (neighbouring blocks share child rows in L2)
+#ifdef KP_STAMPS
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+    const unsigned long long st_real0 = __builtin_amdgcn_s_memrealtime(), st_t0 = st_prev;
+#endif
     uint32_t widx = blockIdx.x;
-    if (P.remap) {
+    if (P.remap) {  // XCD-contiguous runs of the level's block list (A/B option)
         const uint32_t nb = gridDim.x, q = nb >> 3, r = nb & 7u, x = blockIdx.x & 7u;
         widx = x * q + (x < r ? x : r) + (blockIdx.x >> 3);
     }
@@ -135,42 +163,56 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
 #pragma unroll
     for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
 
-    // LDS: st[Bpad][NL] f32 (lanes interleaved) | cd[NL][Bpad] u8 argmin codes | cm[Bpad] CT | cu[Bpad] CT |
-    //      hp[] | pw[t][16]   (Bpad is a multiple of 16, so every carve stays 16-byte aligned)
+    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | pw[t][16] | lm[t][16]
+    //      (count-table scratch aliases st, which the gather fills afterwards; every carve
+    //       offset is a multiple of 16 bytes)
+    const size_t st_bytes = (size_t)NL * Bpad * 4, scr_bytes = (size_t)P.pscratch_entries * 4 * sizeof(CT);
     float *st = reinterpret_cast<float *>(smem);
-    uint8_t *cd = smem + (size_t)NL * Bpad * 4;
-    CT *cm = reinterpret_cast<CT *>(cd + (size_t)NL * Bpad);
-    CT *cu = cm + Bpad;
-    kp_hpair *hp = reinterpret_cast<kp_hpair *>(cu + Bpad);
+    CT *ptab = reinterpret_cast<CT *>(smem + (st_bytes > scr_bytes ? st_bytes : ((scr_bytes + 15) & ~(size_t)15)));
+    kp_hpair *hp = reinterpret_cast<kp_hpair *>(ptab + (((size_t)P.ptab_entries * 2 + 3) & ~(size_t)3));
     uint64_t *pw = reinterpret_cast<uint64_t *>(hp + (g.kh * 7 + 1));
+    uint8_t *lm = reinterpret_cast<uint8_t *>(pw + g.t * 16);
+#ifdef KP_STAMPS
+    unsigned long long *st_lds = reinterpret_cast<unsigned long long *>(lm + ((g.t * 16 + 15) & ~15));
+    if (threadIdx.x < 32) st_lds[threadIdx.x] = 0;
+#endif
 
     const CT *K = reinterpret_cast<const CT *>(P.K);
-    const int np = (P.dbg & 1) ? 0 : kp_high_pair_count(g, P.T.tabs, h);  // wave-uniform
+    // the block's high split pairs, scan order (kp_high_pairs): digits come packed from the
+    // plan (no 64-bit division), counts per position are uniform loads, and wave 0 writes
+    // one pair per lane
+    const uint64_t hd = P.T.hdig[P.hbase + widx];
+    int np = 0;
+    if (!(P.dbg & 1))
+        for (int i = 0; i < g.kh; ++i) np += P.T.tabs[g.t + i].np[(hd >> (4 * i)) & 15u];
     const uint64_t rowstride = (uint64_t)g.Ltot * Bpad;
-    if (threadIdx.x == 0) {
-        kp_high_pairs(g, P.T.tabs, h, hp);
-        for (int p = 0; p < np; ++p) {  // child rows as element offsets of lane 0
-            hp[p].h1 *= rowstride;
-            hp[p].h2 *= rowstride;
+    for (int p = (int)threadIdx.x; threadIdx.x < 64 && p < np; p += 64) {  // wave 0
+        int rem = p, i = 0;
+        uint32_t d = 0;
+        for (; i < g.kh; ++i) {
+            d = (uint32_t)(hd >> (4 * i)) & 15u;
+            const int npi = P.T.tabs[g.t + i].np[d];
+            if (rem < npi) break;
+            rem -= npi;
         }
+        const kp_postab &T = P.T.tabs[g.t + i];
+        hp[p].h1 = (h - (uint64_t)(d - T.pa[d][rem]) * g.hcg[i]) * rowstride;  // child rows as element
+        hp[p].h2 = (h - (uint64_t)(d - T.pb[d][rem]) * g.hcg[i]) * rowstride;  // offsets of lane 0
+        hp[p].code = (uint32_t)(((g.t + i) << 3) | rem);
     }
-    {
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(P.T.pw);
-        uint32_t *dst = reinterpret_cast<uint32_t *>(pw);
-        const uint32_t words = (uint32_t)g.t * 32u;
-        for (uint32_t e = threadIdx.x; e < words; e += blockDim.x) dst[e] = src[e];
-    }
-    // train counts of the block's k-mer-low cells; the level loop aggregates the rest
-    for (uint32_t kl = threadIdx.x; kl < g.n_kl; kl += blockDim.x) {
-        const kp_cnt c = kp_kl_counts<CT>(g, K, h, kl, fold);
-        const uint32_t l = P.T.kl2l[kl];
-        cm[l] = (CT)c.mtr;
-        cu[l] = (CT)c.utr;
-    }
-    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 32u; e += blockDim.x)
+        reinterpret_cast<uint32_t *>(pw)[e] = reinterpret_cast<const uint32_t *>(P.T.pw)[e];
+    for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 16u; e += blockDim.x) lm[e] = P.T.lowmask[e];
+    __syncthreads();  // lm is read by every thread below
 
-    // ---- phase 1: high-position splits, gathered as whole child-block rows ----
-    // winner value -> LDS (interleaved), winner code -> global C directly
+    // ---- separable count tables (train counts of the group fold), kp_core.h ----
+    kp_build_count_table<CT>(g, K, h, fold, lm, reinterpret_cast<CT *>(smem),
+                             reinterpret_cast<CT *>(smem) + (size_t)P.pscratch_entries * 2, ptab, threadIdx.x,
+                             blockDim.x, [] { __syncthreads(); });
+    __syncthreads();
+    KP_STAMP(0);
+
+    // ---- gather: high-position splits, as whole child-block rows (value only) ----
     const uint32_t nch = Bpad / 4;
     for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
         const uint32_t ll = item / nch, c = item % nch;
@@ -178,7 +220,6 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         const float *base = P.S + lrow;
         float4 best = make_float4(__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf(),
                                   __builtin_huge_valf());
-        uint32_t c0 = KP_NONE, c1 = KP_NONE, c2 = KP_NONE, c3 = KP_NONE;
         int p = 0;
         for (; p + 4 <= np; p += 4) {
             const float4 a0 = *reinterpret_cast<const float4 *>(base + hp[p].h1);
@@ -189,26 +230,26 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
             const float4 b2 = *reinterpret_cast<const float4 *>(base + hp[p + 2].h2);
             const float4 a3 = *reinterpret_cast<const float4 *>(base + hp[p + 3].h1);
             const float4 b3 = *reinterpret_cast<const float4 *>(base + hp[p + 3].h2);
-            kp_min4(best, c0, c1, c2, c3, a0, b0, hp[p].code);
-            kp_min4(best, c0, c1, c2, c3, a1, b1, hp[p + 1].code);
-            kp_min4(best, c0, c1, c2, c3, a2, b2, hp[p + 2].code);
-            kp_min4(best, c0, c1, c2, c3, a3, b3, hp[p + 3].code);
+            kp_min4v(best, a0, b0);
+            kp_min4v(best, a1, b1);
+            kp_min4v(best, a2, b2);
+            kp_min4v(best, a3, b3);
         }
         for (; p < np; ++p) {
             const float4 a0 = *reinterpret_cast<const float4 *>(base + hp[p].h1);
             const float4 b0 = *reinterpret_cast<const float4 *>(base + hp[p].h2);
-            kp_min4(best, c0, c1, c2, c3, a0, b0, hp[p].code);
+            kp_min4v(best, a0, b0);
         }
         float *sl = st + (size_t)(4 * c) * NL + ll;
         sl[0] = best.x;
         sl[NL] = best.y;
         sl[2 * NL] = best.z;
         sl[3 * NL] = best.w;
-        *reinterpret_cast<uint32_t *>(cd + (size_t)ll * Bpad + 4 * c) = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
     }
     __syncthreads();
+    KP_STAMP(1);
 
-    // ---- phase 2: low levels inside the block ----
+    // ---- levels: low cells inside the block, level by level ----
     // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
     // the next level's descriptors are loaded while the current level computes
     const bool high_zero = (P.H == 0);
@@ -238,26 +279,11 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
             const int q = (int)threadIdx.x + k * (int)blockDim.x;
             if (q < cnt) {
                 const uint32_t l = cur[k].x & 0xFFFFu;
-                const uint32_t l1 = cur[k].x >> 16, l2 = cur[k].y & 0xFFFFu;
                 const uint32_t info = cur[k].z;
-                CT mt, ut;
-                if (lam == 0) {
-                    mt = cm[l];
-                    ut = cu[l];
-                } else if (P.dbg & 32) {  // timing ablation: no count recurrence
-                    mt = (CT)l1;
-                    ut = (CT)l2;
-                } else {
-                    // count recurrence on the first split (the reference's M_mem/U_mem rows)
-                    mt = cm[l1] + cm[l2];
-                    ut = cu[l1] + cu[l2];
-                    cm[l] = mt;
-                    cu[l] = ut;
-                }
+                // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
                 kp_single_ctx sc;
+                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
                 sc.kmer = high_zero && lam == 0;
-                sc.c.mtr = (uint64_t)mt;
-                sc.c.utr = (uint64_t)ut;
                 sc.c.mte = sc.c.ute = 0;
                 sc.logp = sc.log1mp = 0.0;
                 if (!sc.kmer && !(P.dbg & 4)) {
@@ -265,93 +291,288 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                     sc.logp = log(pr);
                     sc.log1mp = log(1.0 - pr);
                 }
-                uint32_t code[NL];
                 if (!(P.dbg & 8)) {
-                    kp_dp_cell_lanes<NL>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta, pen,
-                                         code);
+                    kp_dp_cell_values<NL>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta, pen);
                 } else {  // timing ablation: no split scan, keep the single term
 #pragma unroll
-                    for (int j = 0; j < NL; ++j) {
+                    for (int j = 0; j < NL; ++j)
                         st[l * NL + j] = (float)kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
-                        code[j] = KP_SINGLE;
-                    }
                 }
-#pragma unroll
-                for (int j = 0; j < NL; ++j)
-                    if (code[j] != KP_NONE) cd[(size_t)j * Bpad + l] = (uint8_t)code[j];
             }
         }
         if (!(P.dbg & 16)) __syncthreads();  // (ablation 16: timing without the level barrier)
+        KP_STAMP(3 + lam);
 #pragma unroll
         for (int k = 0; k < KP_IPT; ++k) cur[k] = nxt[k];
     }
 
-    // ---- phase 3: store the block's train rows ----
+    // ---- store the block's score rows ----
     for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
         const uint32_t ll = item / nch, c = item % nch;
         const float *sl = st + (size_t)(4 * c) * NL + ll;
         *reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c) =
             make_float4(sl[0], sl[NL], sl[2 * NL], sl[3 * NL]);
     }
-    // ... and its argmin codes, 16 per store
-    const uint32_t nc16 = Bpad / 16;
-    for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nc16; item += blockDim.x) {
-        const uint32_t ll = item / nc16, c = item % nc16;
-        *reinterpret_cast<uint4 *>(P.C + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 16 * c) =
-            *reinterpret_cast<const uint4 *>(cd + (size_t)ll * Bpad + 16 * c);
+    KP_STAMP(2);
+#ifdef KP_STAMPS
+    if (threadIdx.x == 0 && P.stamps) {
+        for (int q = 0; q < 30; ++q)
+            if (st_lds[q]) atomicAdd(P.stamps + q, st_lds[q]);
+        atomicAdd(P.stamps + 30, __builtin_amdgcn_s_memtime() - st_t0);
+        atomicAdd(P.stamps + 31, __builtin_amdgcn_s_memrealtime() - st_real0);
     }
+#endif
 }
+
+// ---------------------------------------------------------------------------
+// breadth-first backtrack
+// ---------------------------------------------------------------------------
+
+struct kp_node {
+    uint64_t x;      // cell
+    uint64_t dig;    // its packed digits
+    uint32_t child;  // first child (the second is child + 1); 0 = leaf
+    uint32_t nleaf;  // leaves of the subtree
+    uint32_t off;    // position of the subtree's first leaf in backtrack order
+    float test;      // test -2LL of the subtree, float32 sums along the tree
+};
+
+struct kp_bt_params {
+    kp_geom g;
+    kp_dev_tables T;
+    const void *K;
+    const float *S;
+    const kp_group_dev *groups;
+    const uint32_t *lanegrp;
+    kp_node *nodes;    // [Ltot][cap]
+    uint32_t cap;
+    uint32_t *cnt;     // [Ltot] nodes allocated
+    uint32_t *dend;    // [Ltot][KP_MAXDEPTH + 1] end of each depth's node range
+    uint32_t *bad;     // [Ltot] 1 = no candidate, 2 = node pool full, 4 = score not reproduced
+    float *root_train, *root_test;
+    uint64_t *nleaves;
+    uint64_t *leaves;  // [Ltot][leafcap]
+    uint64_t leafcap;
+    int depth;
+    int maxdepth;
+};
 
 __device__ inline uint64_t kp_wave_sum(uint64_t v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
     return v;
 }
 
-// test -2LL of a leaf cell: the wave splits the leaf's k-mer-low rows, then reduces
-template <typename CT>
-__device__ inline float kp_leaf_test_wave(const kp_geom &g, const kp_dev_tables &T, const CT *K, uint64_t x, int fold,
-                                          double alpha, double beta) {
-    const uint64_t h = x / g.B;
-    const uint32_t l = (uint32_t)(x % g.B);
-    const uint32_t b = T.klofs[l], e = T.klofs[l + 1];
-    uint64_t mtr = 0, utr = 0, mte = 0, ute = 0;
-    for (uint32_t q = b + (threadIdx.x & 63u); q < e; q += 64) {
-        const kp_cnt c = kp_kl_counts<CT>(g, K, h, T.kllist[q], fold);
-        mtr += c.mtr; utr += c.utr; mte += c.mte; ute += c.ute;
-    }
-    kp_cnt c;
-    c.mtr = kp_wave_sum(mtr);
-    c.utr = kp_wave_sum(utr);
-    c.mte = kp_wave_sum(mte);
-    c.ute = kp_wave_sum(ute);
-    if (fold < 0) return 0.0f;
-    if (kp_is_kmer(g, h, T.lowinfo[l])) return kp_kmer_test(c, alpha, beta);
-    const double p = kp_rate(c, alpha, beta);
-    return kp_single_test(c, log(p), log(1.0 - p));
+__host__ __device__ inline uint64_t kp_s_off(const kp_geom &g, uint64_t h, uint32_t lane, uint32_t l) {
+    return (h * g.Ltot + lane) * (uint64_t)g.Bpad + l;
 }
 
-// one wave per lane: the DFS runs in lockstep in all 64 threads (uniform control flow)
+__global__ void kp_bt_init(kp_bt_params P, uint64_t root_x, uint64_t root_dig) {
+    const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= P.g.Ltot) return;
+    kp_node *N = P.nodes + (uint64_t)lane * P.cap;
+    N[0].x = root_x;
+    N[0].dig = root_dig;
+    N[0].child = 0;
+    N[0].nleaf = 0;
+    N[0].off = 0;
+    N[0].test = 0.0f;
+    P.cnt[lane] = 1;
+    P.dend[(uint64_t)lane * (KP_MAXDEPTH + 1)] = 1;
+    P.bad[lane] = 0;
+}
+
+__global__ void kp_bt_advance(kp_bt_params P) {
+    const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lane >= P.g.Ltot) return;
+    P.dend[(uint64_t)lane * (KP_MAXDEPTH + 1) + P.depth + 1] = P.cnt[lane];
+}
+
+// one wave per node of depth P.depth; grid (waves, lanes)
 template <typename CT>
-__global__ void __launch_bounds__(64) kp_backtrack_kernel(kp_geom g, kp_dev_tables T, const CT *K, const float *S,
-                                                          const uint8_t *C, const kp_group_dev *groups,
-                                                          const uint32_t *lanegrp, float *root_train,
-                                                          float *root_test, uint64_t *nleaves, uint32_t *bad,
-                                                          uint64_t *leaves, uint64_t cap) {
-    const uint32_t lane = blockIdx.x;
-    const kp_group_dev *G = groups + lanegrp[lane];
+__global__ void __launch_bounds__(256) kp_bt_level(kp_bt_params P) {
+    const kp_geom &g = P.g;
+    const uint32_t lane = blockIdx.y;
+    const uint32_t lid = threadIdx.x & 63u;
+    const uint32_t *de = P.dend + (uint64_t)lane * (KP_MAXDEPTH + 1);
+    const uint32_t lo = P.depth ? de[P.depth - 1] : 0u, hi = de[P.depth];
+    const kp_group_dev *G = P.groups + P.lanegrp[lane];
     const int fold = G->fold;
     const double alpha = G->alpha, beta = G->beta;
-    uint64_t n = 0;
-    uint32_t err = 0;
-    auto leaf = [&](uint64_t x) { return kp_leaf_test_wave<CT>(g, T, K, x, fold, alpha, beta); };
-    const bool writer = threadIdx.x == 0;
-    float t = kp_backtrack_lane(g, T.tabs, C, lane, leaf, writer && leaves ? leaves + (uint64_t)lane * cap : nullptr,
-                                cap, &n, &err);
-    if (writer) {
-        root_train[lane] = S[kp_lane_row(g, g.nblocks - 1, lane) + (g.B - 1)];
-        root_test[lane] = t;
-        nleaves[lane] = n;
-        bad[lane] = err;
+    const double pen = G->pen[lane - (uint32_t)G->lane0];
+    const CT *K = reinterpret_cast<const CT *>(P.K);
+    kp_node *N = P.nodes + (uint64_t)lane * P.cap;
+    const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t n = lo + ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); n < hi; n += nw) {
+        const uint64_t x = N[n].x, dig = N[n].dig;
+        const uint64_t h = x / g.B;
+        const uint32_t l = (uint32_t)(x % g.B);
+        const bool kmer = kp_dig_is_kmer(g, dig);
+        // counts: the wave splits the k-mer-low rows of the cell, then reduces
+        uint64_t mtr = 0, utr = 0, mte = 0, ute = 0;
+        const uint32_t q0 = P.T.klofs[l], q1 = P.T.klofs[l + 1];
+        for (uint32_t q = q0 + lid; q < q1; q += 64) {
+            const kp_cnt c = kp_kl_counts<CT>(g, K, h, P.T.kllist[q], fold);
+            mtr += c.mtr; utr += c.utr; mte += c.mte; ute += c.ute;
+        }
+        kp_cnt c;
+        c.mtr = kp_wave_sum(mtr);
+        c.utr = kp_wave_sum(utr);
+        c.mte = kp_wave_sum(mte);
+        c.ute = kp_wave_sum(ute);
+        // split candidates: one (position, pair) per lane, scan order = code order
+        float best = __builtin_huge_valf();
+        uint32_t code = KP_NONE;
+        if (!kmer) {
+            uint32_t npt = 0;
+            for (int i = 0; i < g.k; ++i) npt += P.T.tabs[i].np[kp_dig(dig, i)];
+            for (uint32_t p = lid; p < npt; p += 64) {
+                uint32_t rem = p, d = 0;
+                int i = 0;
+                for (; i < g.k; ++i) {
+                    d = kp_dig(dig, i);
+                    const uint32_t npi = P.T.tabs[i].np[d];
+                    if (rem < npi) break;
+                    rem -= npi;
+                }
+                const kp_postab &T = P.T.tabs[i];
+                const uint32_t da = d - T.pa[d][rem], db = d - T.pb[d][rem];
+                uint64_t o1, o2;
+                if (i < g.t) {
+                    const uint32_t cg = (uint32_t)g.cgl[i];
+                    o1 = kp_s_off(g, h, lane, l - da * cg);
+                    o2 = kp_s_off(g, h, lane, l - db * cg);
+                } else {
+                    o1 = kp_s_off(g, h - (uint64_t)da * g.hcg[i - g.t], lane, l);
+                    o2 = kp_s_off(g, h - (uint64_t)db * g.hcg[i - g.t], lane, l);
+                }
+                const float v = P.S[o1] + P.S[o2];
+                if (v < best) {  // a lane sees its pairs in increasing code order
+                    best = v;
+                    code = (uint32_t)((i << 3) | rem);
+                }
+            }
+            // first minimum over the wave: smaller value, then smaller code (= earlier in scan)
+            for (int off = 32; off > 0; off >>= 1) {
+                const float ob = __shfl_xor(best, off, 64);
+                const uint32_t oc = __shfl_xor(code, off, 64);
+                if (ob < best || (ob == best && oc < code)) {
+                    best = ob;
+                    code = oc;
+                }
+            }
+        }
+        // single pattern term; the stored score must be reproduced exactly
+        float value;
+        float test = 0.0f;
+        if (kmer) {
+            value = kp_kmer_train(c, alpha, beta, pen);
+            code = KP_SINGLE;
+            if (fold >= 0) test = kp_kmer_test(c, alpha, beta);
+        } else {
+            const double pr = kp_rate(c, alpha, beta);
+            const double lp = log(pr), l1p = log(1.0 - pr);
+            const double s = kp_single_train(c, lp, l1p, pen);
+            value = best;
+            if (s < (double)best) {
+                value = (float)s;
+                code = KP_SINGLE;
+            }
+            if (code == KP_SINGLE && fold >= 0) test = kp_single_test(c, lp, l1p);
+        }
+        if (lid == 0) {
+            const float stored = P.S[kp_s_off(g, h, lane, l)];
+            const bool same = (__float_as_uint(stored) == __float_as_uint(value)) || (stored != stored && value != value);
+            uint32_t err = same ? 0u : 4u;
+            if (code == KP_SINGLE) {
+                N[n].child = 0;
+                N[n].test = test;
+            } else if (code == KP_NONE) {
+                err |= 1u;
+                N[n].child = 0;
+                N[n].test = 0.0f;
+            } else {
+                const uint32_t base = atomicAdd(P.cnt + lane, 2u);
+                if (base + 2 > P.cap) {
+                    err |= 2u;
+                    N[n].child = 0;
+                } else {
+                    const int i = (int)(code >> 3), j = (int)(code & 7u);
+                    const uint32_t d = kp_dig(dig, i);
+                    const kp_postab &T = P.T.tabs[i];
+                    const uint64_t clear = ~(15ull << (4 * i));
+                    kp_node a, b;
+                    a.x = x - (uint64_t)(d - T.pa[d][j]) * g.cgl[i];
+                    a.dig = (dig & clear) | ((uint64_t)T.pa[d][j] << (4 * i));
+                    b.x = x - (uint64_t)(d - T.pb[d][j]) * g.cgl[i];
+                    b.dig = (dig & clear) | ((uint64_t)T.pb[d][j] << (4 * i));
+                    a.child = b.child = 0;
+                    a.nleaf = b.nleaf = 0;
+                    a.off = b.off = 0;
+                    a.test = b.test = 0.0f;
+                    N[base] = a;
+                    N[base + 1] = b;
+                    N[n].child = base;
+                }
+            }
+            if (err) atomicOr(P.bad + lane, err);
+        }
+    }
+}
+
+// one workgroup per lane: float32 test sums bottom-up, then leaf order top-down
+__global__ void __launch_bounds__(256) kp_bt_finish(kp_bt_params P) {
+    const kp_geom &g = P.g;
+    const uint32_t lane = blockIdx.x;
+    const uint32_t *de = P.dend + (uint64_t)lane * (KP_MAXDEPTH + 1);
+    kp_node *N = P.nodes + (uint64_t)lane * P.cap;
+    for (int d = P.maxdepth; d >= 0; --d) {
+        const uint32_t lo = d ? de[d - 1] : 0u, hi = de[d];
+        for (uint32_t n = lo + threadIdx.x; n < hi; n += blockDim.x) {
+            const uint32_t c = N[n].child;
+            if (c) {
+                N[n].test = N[c].test + N[c + 1].test;  // test[c1] + test[c2] (CV :47)
+                N[n].nleaf = N[c].nleaf + N[c + 1].nleaf;
+            } else {
+                N[n].nleaf = 1;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) N[0].off = 0;
+    __syncthreads();
+    uint64_t *leaves = P.leaves + (uint64_t)lane * P.leafcap;
+    for (int d = 0; d <= P.maxdepth; ++d) {
+        const uint32_t lo = d ? de[d - 1] : 0u, hi = de[d];
+        for (uint32_t n = lo + threadIdx.x; n < hi; n += blockDim.x) {
+            const uint32_t c = N[n].child, off = N[n].off;
+            if (c) {
+                N[c].off = off;
+                N[c + 1].off = off + N[c].nleaf;
+            } else if (off < P.leafcap) {
+                leaves[off] = N[n].x;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        P.root_train[lane] = P.S[kp_s_off(g, g.nblocks - 1, lane, g.B - 1)];
+        P.root_test[lane] = N[0].test;
+        P.nleaves[lane] = N[0].nleaf;
+    }
+}
+
+// argmin code of every cell of one lane (parity dumps): the sequential decision of kp_core.h
+template <typename CT>
+__global__ void kp_codes_kernel(kp_geom g, kp_dev_tables T, const CT *K, const float *S, kp_group_dev G,
+                                uint32_t lane, double pen, uint8_t *code) {
+    const uint64_t npat = g.nblocks * g.B;
+    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < npat;
+         x += (uint64_t)gridDim.x * blockDim.x) {
+        const kp_cnt c = kp_cell_counts<CT>(g, T.klofs, T.kllist, K, x, G.fold);
+        const uint64_t dig = kp_cell_digits(g, x);
+        auto score = [&](uint64_t y) { return S[kp_s_off(g, y / g.B, lane, (uint32_t)(y % g.B))]; };
+        float v;
+        code[x] = (uint8_t)kp_cell_decide(g, T.tabs, x, dig, score, c, G.alpha, G.beta, pen, &v);
     }
 }
 
@@ -386,30 +607,35 @@ struct kp_plan {
     // device tables
     kp_postab *d_tabs = nullptr;
     uint32_t *d_lowinfo = nullptr;
-    uint16_t *d_lorder = nullptr;
     int32_t *d_loff = nullptr;
     uint32_t *d_klofs = nullptr;
     uint16_t *d_kllist = nullptr;
     uint32_t *d_hlist = nullptr;
     kp_lowdesc *d_ldesc = nullptr;
-    uint16_t *d_kl2l = nullptr;
     uint64_t *d_pw = nullptr;
+    uint64_t *d_hdig = nullptr;
+    uint8_t *d_lowmask = nullptr;
     // counts
     void *d_K = nullptr;
     int nf = 0;
     int ct_bytes = 0;
     // lanes
     float *d_S = nullptr;
-    uint8_t *d_C = nullptr;
     uint64_t lanes_cap = 0;
+    kp_node *d_nodes = nullptr;
+    uint32_t node_cap = 0;  // nodes per lane
     kp_group_dev *d_groups = nullptr;
     uint32_t *d_lanegrp = nullptr;
     float *d_rtrain = nullptr, *d_rtest = nullptr;
     uint64_t *d_nleaves = nullptr;
     uint32_t *d_bad = nullptr;
+    uint32_t *d_cnt = nullptr;
+    uint32_t *d_dend = nullptr;
     uint64_t *d_leaves = nullptr;
     uint64_t small_cap = 0;  // lanes the small buffers above can hold
     uint32_t last_ltot = 0;
+    std::vector<kp_group_dev> last_groups;  // device groups of the last pass (dump)
+    std::vector<uint32_t> last_lanegrp;
     kp_pass_stats stats{};
 };
 
@@ -417,19 +643,19 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     kp_dev_tables T;
     T.tabs = p->d_tabs;
     T.lowinfo = p->d_lowinfo;
-    T.lorder = p->d_lorder;
     T.loff = p->d_loff;
     T.klofs = p->d_klofs;
     T.kllist = p->d_kllist;
     T.hlist = p->d_hlist;
     T.ldesc = p->d_ldesc;
-    T.kl2l = p->d_kl2l;
     T.pw = p->d_pw;
+    T.hdig = p->d_hdig;
+    T.lowmask = p->d_lowmask;
     return T;
 }
 
 template <typename T>
-static int upload(kp_plan *p, T **dptr, const std::vector<T> &v) {
+static int upload(T **dptr, const std::vector<T> &v) {
     size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
     KP_HIP(hipMalloc(reinterpret_cast<void **>(dptr), bytes));
     if (!v.empty()) KP_HIP(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
@@ -439,6 +665,9 @@ static int upload(kp_plan *p, T **dptr, const std::vector<T> &v) {
 static void dfree(void *p) {
     if (p) (void)hipFree(p);
 }
+
+// nodes of one lane's backtrack tree: at most 2 * leaves - 1 <= 2 * n_kmers - 1
+static uint32_t node_cap_of(const kp::host_plan &hp) { return (uint32_t)(2 * hp.n_kmers + 2); }
 
 extern "C" {
 
@@ -497,11 +726,11 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
         return fail(KP_E_ARG, err);
     }
     int rc;
-    if ((rc = upload(p, &p->d_tabs, p->hp.tabs)) || (rc = upload(p, &p->d_lowinfo, p->hp.lowinfo)) ||
-        (rc = upload(p, &p->d_lorder, p->hp.lorder)) || (rc = upload(p, &p->d_loff, p->hp.loff)) ||
-        (rc = upload(p, &p->d_klofs, p->hp.klofs)) || (rc = upload(p, &p->d_kllist, p->hp.kllist)) ||
-        (rc = upload(p, &p->d_hlist, p->hp.hlist)) || (rc = upload(p, &p->d_ldesc, p->hp.ldesc)) ||
-        (rc = upload(p, &p->d_kl2l, p->hp.kl2l)) || (rc = upload(p, &p->d_pw, p->hp.pw))) {
+    if ((rc = upload(&p->d_tabs, p->hp.tabs)) || (rc = upload(&p->d_lowinfo, p->hp.lowinfo)) ||
+        (rc = upload(&p->d_loff, p->hp.loff)) || (rc = upload(&p->d_klofs, p->hp.klofs)) ||
+        (rc = upload(&p->d_kllist, p->hp.kllist)) || (rc = upload(&p->d_hlist, p->hp.hlist)) ||
+        (rc = upload(&p->d_ldesc, p->hp.ldesc)) || (rc = upload(&p->d_pw, p->hp.pw)) ||
+        (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_lowmask, p->hp.lowmask))) {
         kp_plan_destroy(p);
         return rc;
     }
@@ -512,10 +741,10 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
 void kp_plan_destroy(kp_plan *p) {
     if (!p) return;
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
-    void *bufs[] = {p->d_tabs, p->d_lowinfo, p->d_lorder, p->d_loff, p->d_klofs, p->d_kllist, p->d_hlist,
-                    p->d_ldesc, p->d_kl2l, p->d_pw,
-                    p->d_K, p->d_S, p->d_C, p->d_groups, p->d_lanegrp, p->d_rtrain, p->d_rtest,
-                    p->d_nleaves, p->d_bad, p->d_leaves};
+    void *bufs[] = {p->d_tabs,    p->d_lowinfo, p->d_loff,   p->d_klofs,   p->d_kllist, p->d_hlist, p->d_ldesc,
+                    p->d_pw,      p->d_hdig,    p->d_lowmask, p->d_K,      p->d_S,      p->d_nodes, p->d_groups,
+                    p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
+                    p->d_leaves};
     for (void *b : bufs) dfree(b);
     delete p;
 }
@@ -534,7 +763,9 @@ int kp_plan_get_info(const kp_plan *p, kp_plan_info *o) {
     o->high_levels = h.hmax + 1;
     o->pairs_total = h.pairs_total;
     o->pairs_high = h.pairs_high;
-    o->bytes_per_lane = h.g.nblocks * (uint64_t)h.g.Bpad * 5;
+    // train scores + backtrack node pool + leaf list
+    o->bytes_per_lane = h.g.nblocks * (uint64_t)h.g.Bpad * 4 + (uint64_t)node_cap_of(h) * sizeof(kp_node) +
+                        h.n_kmers * 8 + 4096;
     return KP_OK;
 }
 
@@ -597,10 +828,18 @@ int kp_set_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers, in
 
 }  // extern "C"
 
+// dynamic LDS of kp_dp_kernel (carve order and rounding exactly as in the kernel)
 static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
     const kp_geom &g = hp.g;
-    return (size_t)nl * g.Bpad * 5 + 2 * (size_t)g.Bpad * ct_bytes + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) +
-           (size_t)g.t * 16 * sizeof(uint64_t) + 16;
+    const size_t st = (size_t)nl * g.Bpad * 4;
+    const size_t scratch = (((size_t)hp.pscratch_entries * 4 * ct_bytes) + 15) & ~(size_t)15;  // 2 build buffers
+    const size_t ptab = ((((size_t)hp.ptab_entries * 2 + 3) & ~(size_t)3)) * ct_bytes;
+    return std::max(st, scratch) + ptab + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) + (size_t)g.t * 16 * 8 +
+           (((size_t)g.t * 16 + 15) & ~(size_t)15) + 16
+#ifdef KP_STAMPS
+           + 32 * sizeof(unsigned long long)
+#endif
+        ;
 }
 
 template <typename CT, int NL>
@@ -632,12 +871,12 @@ static int launch_dp_nl(int nl, kp_ctx *c, const kp_dp_params &P, unsigned nb, u
 static int dp_threads() {
     const char *e = getenv("KP_DP_THREADS");
     int v = e ? atoi(e) : 512;
-    return (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) ? v : 256;
+    return (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) ? v : 512;
 }
 
 static int lanes_per_wg_default() {
     const char *e = getenv("KP_LANES_PER_WG");
-    int v = e ? atoi(e) : 3;
+    int v = e ? atoi(e) : 5;
     return std::min(std::max(v, 1), KP_GROUP_LANES);
 }
 
@@ -649,12 +888,13 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     const kp::host_plan &hp = p->hp;
     kp_geom g = hp.g;
     g.nf = p->nf;
-    // split user groups into device groups that fit the LDS budget
+    // split user groups into device groups that fit two workgroups per CU in LDS when
+    // possible (LDS is the occupancy limit of the sweep)
     int per_wg = lanes_per_wg_default();
-    while (per_wg > 1 && dp_lds_bytes(hp, per_wg, sizeof(CT)) > c->lds_max) --per_wg;
+    const size_t lds_two = std::min<size_t>(c->lds_max, 160u * 1024u / 2u);
+    while (per_wg > 1 && dp_lds_bytes(hp, per_wg, sizeof(CT)) > lds_two) --per_wg;
     if (dp_lds_bytes(hp, 1, sizeof(CT)) > c->lds_max) return fail(KP_E_ARG, "block does not fit LDS");
     std::vector<kp_group_dev> dg;
-    std::vector<uint32_t> lanegrp;
     uint32_t lane = 0;
     for (int i = 0; i < n_groups; ++i) {
         const kp_group &u = groups[i];
@@ -669,7 +909,6 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
             d.alpha = u.alpha;
             d.beta = u.beta;
             for (int j = 0; j < d.nl; ++j) d.pen[j] = u.penalty[s + j];
-            for (int j = 0; j < d.nl; ++j) lanegrp.push_back((uint32_t)dg.size());
             lane += (uint32_t)d.nl;
             dg.push_back(d);
         }
@@ -678,7 +917,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     g.Ltot = Ltot;
     // launch classes: device groups with equal lane counts share one launch per level
     std::stable_sort(dg.begin(), dg.end(), [](const kp_group_dev &a, const kp_group_dev &b) { return a.nl > b.nl; });
-    lanegrp.assign(Ltot, 0);
+    std::vector<uint32_t> lanegrp(Ltot, 0);
     for (size_t i = 0; i < dg.size(); ++i)
         for (int j = 0; j < dg[i].nl; ++j) lanegrp[dg[i].lane0 + j] = (uint32_t)i;
     // threads per workgroup: every level of the block must fit KP_IPT cells per thread
@@ -687,25 +926,28 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     int threads = dp_threads();
     while (threads < KP_DP_MAX_THREADS && threads * KP_IPT < max_level_cells) threads *= 2;
     if (threads * KP_IPT < max_level_cells) return fail(KP_E_ARG, "block level too wide for one workgroup");
-    // lane storage
+    // lane storage: scores, and the backtrack node pool
+    const uint32_t ncap = node_cap_of(hp);
     if (Ltot > p->lanes_cap) {
         dfree(p->d_S);
-        dfree(p->d_C);
+        dfree(p->d_nodes);
         p->d_S = nullptr;
-        p->d_C = nullptr;
+        p->d_nodes = nullptr;
         p->lanes_cap = 0;
-        size_t sb = g.nblocks * (size_t)Ltot * g.Bpad * 4, cb = g.nblocks * (size_t)Ltot * g.Bpad;
+        size_t sb = g.nblocks * (size_t)Ltot * g.Bpad * 4, nb = (size_t)Ltot * ncap * sizeof(kp_node);
         size_t fr = 0, tot = 0;
         KP_HIP(hipMemGetInfo(&fr, &tot));
-        if (sb + cb + (256u << 20) > fr)
-            return fail(KP_E_NOMEM, "lanes need " + std::to_string(sb + cb) + " bytes, free " + std::to_string(fr));
+        if (sb + nb + (256u << 20) > fr)
+            return fail(KP_E_NOMEM, "lanes need " + std::to_string(sb + nb) + " bytes, free " + std::to_string(fr));
         KP_HIP(hipMalloc(&p->d_S, sb));
-        KP_HIP(hipMalloc(&p->d_C, cb));
+        KP_HIP(hipMalloc(&p->d_nodes, nb));
         KP_HIP(hipMemsetAsync(p->d_S, 0, sb, c->stream));
         p->lanes_cap = Ltot;
+        p->node_cap = ncap;
     }
     if (Ltot > p->small_cap || dg.size() > p->small_cap) {
-        void *bufs[] = {p->d_groups, p->d_lanegrp, p->d_rtrain, p->d_rtest, p->d_nleaves, p->d_bad, p->d_leaves};
+        void *bufs[] = {p->d_groups, p->d_lanegrp, p->d_rtrain, p->d_rtest, p->d_nleaves,
+                        p->d_bad,    p->d_cnt,     p->d_dend,   p->d_leaves};
         for (void *b : bufs) dfree(b);
         uint64_t cap = std::max<uint64_t>(Ltot, 64);
         KP_HIP(hipMalloc(&p->d_groups, cap * sizeof(kp_group_dev)));
@@ -714,6 +956,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         KP_HIP(hipMalloc(&p->d_rtest, cap * sizeof(float)));
         KP_HIP(hipMalloc(&p->d_nleaves, cap * sizeof(uint64_t)));
         KP_HIP(hipMalloc(&p->d_bad, cap * sizeof(uint32_t)));
+        KP_HIP(hipMalloc(&p->d_cnt, cap * sizeof(uint32_t)));
+        KP_HIP(hipMalloc(&p->d_dend, cap * (KP_MAXDEPTH + 1) * sizeof(uint32_t)));
         KP_HIP(hipMalloc(&p->d_leaves, cap * hp.n_kmers * sizeof(uint64_t)));
         p->small_cap = cap;
     }
@@ -722,15 +966,24 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
                           c->stream));
 
     kp_dp_params P;
+    memset(&P, 0, sizeof(P));
     P.g = g;
     P.T = tables_of(p);
     P.K = p->d_K;
     P.S = p->d_S;
-    P.C = p->d_C;
     P.groups = p->d_groups;
     P.lmax = hp.lmax;
+    P.ptab_entries = hp.ptab_entries;
+    P.pscratch_entries = hp.pscratch_entries;
     P.dbg = getenv("KP_DEBUG_SKIP") ? atoi(getenv("KP_DEBUG_SKIP")) : 0;
     P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 0;
+    P.stamps = nullptr;
+#ifdef KP_STAMPS
+    static unsigned long long *d_stamps = nullptr;
+    if (!d_stamps) KP_HIP(hipMalloc(&d_stamps, 32 * sizeof(unsigned long long)));
+    KP_HIP(hipMemsetAsync(d_stamps, 0, 32 * sizeof(unsigned long long), c->stream));
+    P.stamps = d_stamps;
+#endif
     KP_HIP(hipEventRecord(c->ev[0], c->stream));
     uint64_t launches = 0;
     for (int H = 0; H <= hp.hmax; ++H) {
@@ -751,29 +1004,78 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         }
     }
     KP_HIP(hipEventRecord(c->ev[1], c->stream));
-    if (!P.dbg) hipLaunchKernelGGL(kp_backtrack_kernel<CT>, dim3(Ltot), dim3(64), 0, c->stream, g, P.T,
-                       reinterpret_cast<const CT *>(p->d_K), p->d_S, p->d_C, p->d_groups, p->d_lanegrp, p->d_rtrain,
-                       p->d_rtest, p->d_nleaves, p->d_bad, p->d_leaves, (uint64_t)hp.n_kmers);
-    KP_HIP(hipGetLastError());
+    // breadth-first backtrack of every lane: depth d holds cells of level <= maxlev - d
+    kp_bt_params B;
+    memset(&B, 0, sizeof(B));
+    B.g = g;
+    B.T = P.T;
+    B.K = p->d_K;
+    B.S = p->d_S;
+    B.groups = p->d_groups;
+    B.lanegrp = p->d_lanegrp;
+    B.nodes = p->d_nodes;
+    B.cap = p->node_cap;
+    B.cnt = p->d_cnt;
+    B.dend = p->d_dend;
+    B.bad = p->d_bad;
+    B.root_train = p->d_rtrain;
+    B.root_test = p->d_rtest;
+    B.nleaves = p->d_nleaves;
+    B.leaves = p->d_leaves;
+    B.leafcap = hp.n_kmers;
+    B.maxdepth = hp.maxlev;
+    const bool bt = !P.dbg;
+    if (bt) {
+        const unsigned lb = (Ltot + 63) / 64;
+        const uint64_t root = hp.npat - 1;
+        hipLaunchKernelGGL(kp_bt_init, dim3(lb), dim3(64), 0, c->stream, B, root, kp_cell_digits(g, root));
+        KP_HIP(hipGetLastError());
+        for (int d = 0; d <= hp.maxlev; ++d) {
+            B.depth = d;
+            hipLaunchKernelGGL(kp_bt_level<CT>, dim3(64, Ltot), dim3(256), 0, c->stream, B);
+            KP_HIP(hipGetLastError());
+            hipLaunchKernelGGL(kp_bt_advance, dim3(lb), dim3(64), 0, c->stream, B);
+            KP_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(kp_bt_finish, dim3(Ltot), dim3(256), 0, c->stream, B);
+        KP_HIP(hipGetLastError());
+    }
     KP_HIP(hipEventRecord(c->ev[2], c->stream));
-    std::vector<uint32_t> bad(Ltot);
+    std::vector<uint32_t> bad(Ltot, 0);
     std::vector<float> rtr(Ltot), rte(Ltot);
     std::vector<uint64_t> nlv(Ltot);
-    KP_HIP(hipMemcpyAsync(rtr.data(), p->d_rtrain, Ltot * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    KP_HIP(hipMemcpyAsync(rte.data(), p->d_rtest, Ltot * sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    KP_HIP(hipMemcpyAsync(nlv.data(), p->d_nleaves, Ltot * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-    KP_HIP(hipMemcpyAsync(bad.data(), p->d_bad, Ltot * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    if (bt) {
+        KP_HIP(hipMemcpyAsync(rtr.data(), p->d_rtrain, Ltot * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        KP_HIP(hipMemcpyAsync(rte.data(), p->d_rtest, Ltot * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        KP_HIP(hipMemcpyAsync(nlv.data(), p->d_nleaves, Ltot * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+        KP_HIP(hipMemcpyAsync(bad.data(), p->d_bad, Ltot * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    }
     KP_HIP(hipStreamSynchronize(c->stream));
     float dp_ms = 0, bt_ms = 0;
     KP_HIP(hipEventElapsedTime(&dp_ms, c->ev[0], c->ev[1]));
+#ifdef KP_STAMPS
+    {
+        unsigned long long hs[32];
+        KP_HIP(hipMemcpy(hs, P.stamps, sizeof(hs), hipMemcpyDeviceToHost));
+        fprintf(stderr, "KP_STAMPS init %.4g gather %.4g store %.4g wg_ticks %.4g wg_real100MHz %.4g levels",
+                (double)hs[0], (double)hs[1], (double)hs[2], (double)hs[30], (double)hs[31]);
+        for (int l = 0; l <= hp.lmax; ++l) fprintf(stderr, " %.4g", (double)hs[3 + l]);
+        fprintf(stderr, "\n");
+    }
+#endif
     KP_HIP(hipEventElapsedTime(&bt_ms, c->ev[1], c->ev[2]));
     for (uint32_t i = 0; i < Ltot; ++i) {
-        if (bad[i] && !P.dbg) return fail(KP_E_PARITY, "argmin tree of lane " + std::to_string(i) + " is broken");
+        if (bad[i])
+            return fail(KP_E_PARITY, "backtrack of lane " + std::to_string(i) + " failed (flags " +
+                                         std::to_string(bad[i]) +
+                                         ": 1 no candidate, 2 node pool, 4 score not reproduced)");
         if (root_train) root_train[i] = rtr[i];
         if (root_test) root_test[i] = rte[i];
         if (n_leaves) n_leaves[i] = nlv[i];
     }
     p->last_ltot = Ltot;
+    p->last_groups = dg;
+    p->last_lanegrp = lanegrp;
     kp_pass_stats &s = p->stats;
     s.dp_ms = dp_ms;
     s.backtrack_ms = bt_ms;
@@ -782,9 +1084,32 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     const double sz = (double)sizeof(CT), npat = (double)hp.npat, nk = (double)hp.n_kmers;
     // 16 B per split pair, 8 B per cell write, 6s per aggregated cell, 2s per k-mer
     s.alg_bytes = (double)Ltot * (16.0 * hp.pairs_total + 8.0 * npat + 6.0 * sz * (npat - nk) + 2.0 * sz * nk);
+    // compulsory HBM bytes of the blocked sweep: high-split gathers (2 x f32) + score writes
     const double padf = (double)g.Bpad / (double)g.B;
-    s.gather_bytes = (double)Ltot * padf * (8.0 * hp.pairs_high + 5.0 * npat);
+    s.gather_bytes = (double)Ltot * padf * (8.0 * hp.pairs_high + 4.0 * npat);
     s.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return KP_OK;
+}
+
+template <typename CT>
+static int run_codes(kp_plan *p, uint32_t lane, uint8_t *code) {
+    kp_ctx *c = p->ctx;
+    const kp::host_plan &hp = p->hp;
+    kp_geom g = hp.g;
+    g.nf = p->nf;
+    g.Ltot = p->last_ltot;
+    const kp_group_dev &G = p->last_groups[p->last_lanegrp[lane]];
+    const double pen = G.pen[lane - (uint32_t)G.lane0];
+    uint8_t *d_code = nullptr;
+    KP_HIP(hipMalloc(&d_code, hp.npat));
+    const unsigned nb = (unsigned)std::min<uint64_t>((hp.npat + 255) / 256, 65535);
+    hipLaunchKernelGGL(kp_codes_kernel<CT>, dim3(nb), dim3(256), 0, c->stream, g, tables_of(p),
+                       reinterpret_cast<const CT *>(p->d_K), p->d_S, G, lane, pen, d_code);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(code, d_code, hp.npat, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree(d_code);
+    if (e != hipSuccess) return fail(KP_E_HIP, std::string("codes kernel: ") + hipGetErrorString(e));
     return KP_OK;
 }
 
@@ -825,19 +1150,15 @@ int kp_dump_lane(kp_plan *p, uint32_t lane, float *score, uint8_t *code) {
     KP_HIP(hipSetDevice(p->ctx->device));
     const kp_geom &g = p->hp.g;
     const uint64_t ltot = p->last_ltot;
-    std::vector<float> rowf(g.Bpad);
-    std::vector<uint8_t> rowc(g.Bpad);
-    for (uint64_t h = 0; h < g.nblocks; ++h) {
-        uint64_t off = (h * ltot + lane) * (uint64_t)g.Bpad;
-        if (score) {
+    if (score) {
+        std::vector<float> rowf(g.Bpad);
+        for (uint64_t h = 0; h < g.nblocks; ++h) {
+            uint64_t off = (h * ltot + lane) * (uint64_t)g.Bpad;
             KP_HIP(hipMemcpy(rowf.data(), p->d_S + off, g.Bpad * sizeof(float), hipMemcpyDeviceToHost));
             memcpy(score + h * g.B, rowf.data(), g.B * sizeof(float));
         }
-        if (code) {
-            KP_HIP(hipMemcpy(rowc.data(), p->d_C + off, g.Bpad, hipMemcpyDeviceToHost));
-            memcpy(code + h * g.B, rowc.data(), g.B);
-        }
     }
+    if (code) return p->ct_bytes == 4 ? run_codes<uint32_t>(p, lane, code) : run_codes<uint64_t>(p, lane, code);
     return KP_OK;
 }
 

@@ -40,6 +40,9 @@ struct host_plan {
     uint64_t n_kmers = 0;
     std::vector<kp_postab> tabs;       // [k]
     std::vector<uint64_t> pw;          // [t][16] pair words of the low positions (kp_pair_word)
+    std::vector<uint8_t> lowmask;      // [t][16] nucleotide-index bit mask of each low digit
+    uint32_t ptab_entries = 0;         // separable count table: cgl[t-1] low prefixes x n[t-1]
+    uint32_t pscratch_entries = 0;     // largest intermediate table of its build
     std::vector<uint32_t> lowinfo;     // [B] packed low digits
     std::vector<uint16_t> lorder;      // [B] low cells sorted by low level
     std::vector<int32_t> loff;         // [lmax + 2]
@@ -48,6 +51,7 @@ struct host_plan {
     std::vector<uint32_t> klofs;       // [B + 1]
     std::vector<uint16_t> kllist;      // k-mer-low cells matching each low cell
     std::vector<uint32_t> hlist;       // [nblocks] blocks sorted by high level
+    std::vector<uint64_t> hdig;        // [nblocks] their high digits, 4 bits per high position
     std::vector<uint64_t> hoff;        // [hmax + 2]
     uint32_t kh_nuc_weight = 0;
     // algorithmic accounting: split pairs summed over all cells
@@ -113,6 +117,29 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     P.pw.assign((size_t)t * 16, 0);
     for (int i = 0; i < t; ++i)
         for (uint32_t d = 0; d < g.r[i]; ++d) P.pw[i * 16 + d] = kp_pair_word(P.tabs[i], d);
+    // nucleotide masks: nucleotide c of general code G has k-mer digit = index of c in code[G]
+    P.lowmask.assign((size_t)t * 16, 0);
+    for (int i = 0; i < t; ++i) {
+        const int gi = iupac_index(P.gp[i]);
+        for (uint32_t d = 0; d < g.r[i]; ++d) {
+            const char *nucs = kNuc[iupac_index(kPerm[gi][d])];
+            uint8_t m = 0;
+            for (const char *c = nucs; *c; ++c) m |= (uint8_t)(1u << (strchr(kNuc[gi], *c) - kNuc[gi]));
+            P.lowmask[i * 16 + d] = m;
+        }
+    }
+    // separable count tables T_s (kp_dp_kernel): digits of positions < s, nucleotides >= s
+    {
+        uint64_t R = 1, mx = 1;
+        for (int s = 0; s < t; ++s) {
+            uint64_t nn = 1;
+            for (int i = s; i < t; ++i) nn *= g.n[i];
+            mx = std::max<uint64_t>(mx, R * nn);
+            if (s < t - 1) R *= g.r[s];
+        }
+        P.ptab_entries = (uint32_t)(R * g.n[t - 1]);
+        P.pscratch_entries = (uint32_t)mx;
+    }
     // low cells: digits, levels, order, matching k-mer-low cells
     uint32_t B = g.B;
     if (B > 0xFFFFu) return "block too large for 16-bit cell ids";
@@ -220,6 +247,13 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     {
         std::vector<uint64_t> fill(P.hoff.begin(), P.hoff.end() - 1);
         for (uint64_t h = 0; h < g.nblocks; ++h) P.hlist[fill[hl[h]]++] = (uint32_t)h;
+    }
+    if (g.kh > 15) return "too many high positions for packed digits";
+    P.hdig.resize(g.nblocks);
+    for (uint64_t q = 0; q < g.nblocks; ++q) {
+        uint64_t h = P.hlist[q], w = 0;
+        for (int i = 0; i < g.kh; ++i) w |= (uint64_t)kp_high_digit(g, h, i) << (4 * i);
+        P.hdig[q] = w;
     }
     // split pairs per position: sum over digits of np, times the other radices
     for (int i = 0; i < k; ++i) {

@@ -21,7 +21,8 @@ import numpy as np
 from .pattern_utils import code_no
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkmerpapa_hip.so")
+# KMERPAPA_LIB selects another build of the same C-ABI (e.g. the -DKP_STAMPS diagnostic build)
+LIB_PATH = os.environ.get("KMERPAPA_LIB") or os.path.join(_HERE, "libkmerpapa_hip.so")
 MAX_GROUP_LANES = 8
 
 _lib = None

@@ -6,6 +6,7 @@
 // and the argmin backtrack against the oracle without a GPU.  It is never loaded by the
 // product package.
 #include <stdint.h>
+#include <math.h>
 #include <string.h>
 
 #include <string>
@@ -17,17 +18,17 @@
 namespace {
 std::string g_err;
 
-void cell_lanes(int nl, const kp_geom &g, const uint64_t *tabs, uint32_t l, uint32_t info, float *st,
-                const kp_single_ctx &sc, double a, double b, const double *pen, uint32_t *code) {
+void cell_values(int nl, const kp_geom &g, const uint64_t *pw, uint32_t l, uint32_t info, float *st,
+                 const kp_single_ctx &sc, double a, double b, const double *pen) {
     switch (nl) {
-        case 1: kp_dp_cell_lanes<1>(g, tabs, l, info, st, sc, a, b, pen, code); break;
-        case 2: kp_dp_cell_lanes<2>(g, tabs, l, info, st, sc, a, b, pen, code); break;
-        case 3: kp_dp_cell_lanes<3>(g, tabs, l, info, st, sc, a, b, pen, code); break;
-        case 4: kp_dp_cell_lanes<4>(g, tabs, l, info, st, sc, a, b, pen, code); break;
-        case 5: kp_dp_cell_lanes<5>(g, tabs, l, info, st, sc, a, b, pen, code); break;
-        case 6: kp_dp_cell_lanes<6>(g, tabs, l, info, st, sc, a, b, pen, code); break;
-        case 7: kp_dp_cell_lanes<7>(g, tabs, l, info, st, sc, a, b, pen, code); break;
-        default: kp_dp_cell_lanes<8>(g, tabs, l, info, st, sc, a, b, pen, code); break;
+        case 1: kp_dp_cell_values<1>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 2: kp_dp_cell_values<2>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 3: kp_dp_cell_values<3>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 4: kp_dp_cell_values<4>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 5: kp_dp_cell_values<5>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 6: kp_dp_cell_values<6>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 7: kp_dp_cell_values<7>(g, pw, l, info, st, sc, a, b, pen); break;
+        default: kp_dp_cell_values<8>(g, pw, l, info, st, sc, a, b, pen); break;
     }
 }
 
@@ -73,11 +74,11 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
             }
         }
     }
+    // the value-only sweep, block by block in the kernel's order and layout
     std::vector<float> S(g.nblocks * (uint64_t)Ltot * g.Bpad, 0.0f);
-    std::vector<uint8_t> C(S.size(), 0);
     std::vector<kp_hpair> hpairs(KP_MAX_HPAIRS);
-    std::vector<kp_cnt> kc(g.n_kl);
     std::vector<float> st;
+    std::vector<CT> bufA((size_t)hp.pscratch_entries * 2), bufB(bufA.size()), ptab((size_t)hp.ptab_entries * 2);
     for (int H = 0; H <= hp.hmax; ++H) {
         for (uint64_t q = hp.hoff[H]; q < hp.hoff[H + 1]; ++q) {
             uint64_t h = hp.hlist[q];
@@ -85,53 +86,37 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
             for (int gi = 0; gi < ngroups; ++gi) {
                 const kp_group_dev &G = groups[gi];
                 st.assign((size_t)G.nl * g.Bpad, 0.0f);  // interleaved [cell][lane], like the kernel
-                for (uint32_t kl = 0; kl < g.n_kl; ++kl) kc[kl] = kp_kl_counts<CT>(g, K.data(), h, kl, G.fold);
-                // phase 1: gather (value -> st, code -> global C)
+                kp_build_count_table<CT>(g, K.data(), h, G.fold, hp.lowmask.data(), bufA.data(), bufB.data(),
+                                         ptab.data(), 0u, 1u, [] {});
+                // gather (values only)
                 for (int ll = 0; ll < G.nl; ++ll) {
                     uint32_t lane = (uint32_t)G.lane0 + ll;
                     for (uint32_t l = 0; l < g.Bpad; ++l) {
                         float best = __builtin_huge_valf();
-                        uint32_t code = KP_NONE;
-                        for (int p = 0; p < np; ++p) {
-                            float v = S[kp_lane_row(g, hpairs[p].h1, lane) + l] + S[kp_lane_row(g, hpairs[p].h2, lane) + l];
-                            if (v < best) { best = v; code = hpairs[p].code; }
-                        }
+                        for (int p = 0; p < np; ++p)
+                            best = fminf(best, S[kp_lane_row(g, hpairs[p].h1, lane) + l] +
+                                                   S[kp_lane_row(g, hpairs[p].h2, lane) + l]);
                         st[(size_t)l * G.nl + ll] = best;
-                        C[kp_lane_row(g, h, lane) + l] = (uint8_t)code;
                     }
                 }
-                // phase 2: levels (same descriptor table, count recurrence and cell function as kp_dp_kernel)
-                std::vector<CT> cm(g.Bpad, 0), cu(g.Bpad, 0);
-                for (uint32_t kl = 0; kl < g.n_kl; ++kl) {
-                    cm[hp.kl2l[kl]] = (CT)kc[kl].mtr;
-                    cu[hp.kl2l[kl]] = (CT)kc[kl].utr;
-                }
+                // levels (same descriptor table, count table and cell function as kp_dp_kernel)
                 for (int lam = 0; lam <= hp.lmax; ++lam) {
                     for (int qq = hp.loff[lam]; qq < hp.loff[lam + 1]; ++qq) {
                         const kp_lowdesc &D = hp.ldesc[qq];
-                        uint32_t l = D.l;
-                        CT mt = lam == 0 ? cm[l] : (CT)(cm[D.l1] + cm[D.l2]);
-                        CT ut = lam == 0 ? cu[l] : (CT)(cu[D.l1] + cu[D.l2]);
-                        cm[l] = mt;
-                        cu[l] = ut;
                         kp_single_ctx sc;
-                        sc.kmer = (H == 0 && lam == 0);
-                        sc.c.mtr = mt;
-                        sc.c.utr = ut;
+                        kp_ptab_counts<CT>(g, hp.lowmask.data(), ptab.data(), D.l, D.info, &sc.c.mtr, &sc.c.utr);
                         sc.c.mte = sc.c.ute = 0;
+                        sc.kmer = (H == 0 && lam == 0);
                         sc.logp = sc.log1mp = 0.0;
                         if (!sc.kmer) {
                             double p = kp_rate(sc.c, G.alpha, G.beta);
                             sc.logp = log(p);
                             sc.log1mp = log(1.0 - p);
                         }
-                        uint32_t code[KP_GROUP_LANES];
-                        cell_lanes(G.nl, g, hp.pw.data(), l, D.info, st.data(), sc, G.alpha, G.beta, G.pen, code);
-                        for (int j = 0; j < G.nl; ++j)
-                            if (code[j] != KP_NONE) C[kp_lane_row(g, h, (uint32_t)G.lane0 + j) + l] = (uint8_t)code[j];
+                        cell_values(G.nl, g, hp.pw.data(), D.l, D.info, st.data(), sc, G.alpha, G.beta, G.pen);
                     }
                 }
-                // phase 3: store
+                // store
                 for (int ll = 0; ll < G.nl; ++ll) {
                     uint64_t row = kp_lane_row(g, h, (uint32_t)G.lane0 + ll);
                     for (uint32_t l = 0; l < g.Bpad; ++l) S[row + l] = st[(size_t)l * G.nl + ll];
@@ -139,35 +124,53 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
             }
         }
     }
-    // backtrack
+    // backtrack: decisions recomputed from the final scores (kp_cell_decide)
     for (int gi = 0; gi < ngroups; ++gi) {
         const kp_group_dev &G = groups[gi];
         for (int ll = 0; ll < G.nl; ++ll) {
-            uint32_t lane = (uint32_t)G.lane0 + ll;
+            const uint32_t lane = (uint32_t)G.lane0 + ll;
+            const double pen = G.pen[ll];
+            auto score = [&](uint64_t y) { return S[kp_lane_row(g, y / g.B, lane) + y % g.B]; };
+            uint32_t mism = 0;
+            auto decide = [&](uint64_t x, uint64_t dig, kp_cnt *c) {
+                *c = kp_cell_counts<CT>(g, hp.klofs.data(), hp.kllist.data(), K.data(), x, G.fold);
+                float v;
+                const uint32_t code = kp_cell_decide(g, hp.tabs.data(), x, dig, score, *c, G.alpha, G.beta, pen, &v);
+                const float sv = score(x);
+                if (memcmp(&sv, &v, 4) != 0 && !(sv != sv && v != v)) mism = 1;
+                return code;
+            };
+            auto leaf = [&](uint64_t x, uint64_t dig, const kp_cnt &c) {
+                (void)x;
+                return kp_leaf_test_term(c, kp_dig_is_kmer(g, dig), G.fold, G.alpha, G.beta);
+            };
             root_train[lane] = S[kp_lane_row(g, g.nblocks - 1, lane) + g.B - 1];
             uint64_t n = 0;
             uint32_t bad = 0;
-            auto leaf = [&](uint64_t x) {
-                return kp_leaf_test<CT>(g, hp.tabs.data(), hp.lowinfo.data(), hp.klofs.data(), hp.kllist.data(),
-                                        K.data(), x, G.fold, G.alpha, G.beta);
-            };
-            root_test[lane] = kp_backtrack_lane(g, hp.tabs.data(), C.data(), lane, leaf,
-                                                leaves ? leaves + lane * hp.n_kmers : nullptr, hp.n_kmers, &n, &bad);
+            root_test[lane] = kp_backtrack_dfs(g, hp.tabs.data(), decide, leaf,
+                                               leaves ? leaves + lane * hp.n_kmers : nullptr, hp.n_kmers, &n, &bad);
             nleaves[lane] = n;
-            if (bad) {
-                g_err = "broken argmin tree";
+            if (bad || mism) {
+                g_err = bad ? "broken argmin tree" : "recomputed decision does not reproduce the stored score";
                 return -5;
+            }
+            if (dump_code) {
+                for (uint64_t x = 0; x < hp.npat; ++x) {
+                    kp_cnt c;
+                    dump_code[(uint64_t)lane * hp.npat + x] = (uint8_t)decide(x, kp_cell_digits(g, x), &c);
+                }
+                if (mism) {
+                    g_err = "recomputed decision does not reproduce the stored score";
+                    return -5;
+                }
             }
         }
     }
-    if (dump_score || dump_code) {
+    if (dump_score) {
         for (uint32_t lane = 0; lane < Ltot; ++lane)
             for (uint64_t h = 0; h < g.nblocks; ++h)
-                for (uint32_t l = 0; l < g.B; ++l) {
-                    uint64_t src = kp_lane_row(g, h, lane) + l, dst = (uint64_t)lane * hp.npat + h * g.B + l;
-                    if (dump_score) dump_score[dst] = S[src];
-                    if (dump_code) dump_code[dst] = C[src];
-                }
+                for (uint32_t l = 0; l < g.B; ++l)
+                    dump_score[(uint64_t)lane * hp.npat + h * g.B + l] = S[kp_lane_row(g, h, lane) + l];
     }
     return 0;
 }
