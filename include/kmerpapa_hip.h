@@ -21,6 +21,8 @@
  *                    handle_pattern :26-78 for every cell) and its root read-out
  *                    :158-163; with fold = -1 the Fit sweep Fit :106-120
  *   kp_fit_leaves    backtrack(gen_pat, ...) Fit :17-24, 121
+ *   kp_fold_split    CV_tools.py sample :5-27 and the fold loop of
+ *                    make_all_folds_contextD_patterns :44-57 (host code, numpy legacy RNG)
  */
 #ifndef KMERPAPA_HIP_H
 #define KMERPAPA_HIP_H
@@ -109,6 +111,14 @@ int kp_fit_leaves(kp_plan *plan, uint32_t lane, uint64_t *leaves, uint64_t cap, 
 /* Debug / parity: copy one lane's train scores and argmin codes, in cell-index order
  * ([npat] each; either pointer may be NULL). */
 int kp_dump_lane(kp_plan *plan, uint32_t lane, float *score, uint8_t *code);
+
+/* Host-only (no GPU needed): the cross-validation fold split of CV_tools.py
+ * make_all_folds_contextD_patterns :44-57 / sample :5-27 with numpy's legacy
+ * RandomState stream.  mt_key[624] / *mt_pos = the MT19937 state of the caller's
+ * RandomState (RandomState.get_state()[1:3]), advanced in place exactly as numpy would.
+ * colors[n] = ball counts per colour; folds[n][nf] receives each colour's fold counts
+ * (folds 0..nf-2 sampled, the last takes the remainder). */
+int kp_fold_split(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uint64_t n, int nf, uint64_t *folds);
 
 #ifdef __cplusplus
 }

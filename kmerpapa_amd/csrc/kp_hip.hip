@@ -36,6 +36,7 @@
 
 #include "../../include/kmerpapa_hip.h"
 #include "kp_core.h"
+#include "kp_folds.h"
 #include "kp_plan.h"
 
 #define KP_DP_MAX_THREADS 1024
@@ -1159,6 +1160,38 @@ int kp_dump_lane(kp_plan *p, uint32_t lane, float *score, uint8_t *code) {
         }
     }
     if (code) return p->ct_bytes == 4 ? run_codes<uint32_t>(p, lane, code) : run_codes<uint64_t>(p, lane, code);
+    return KP_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int kp_fold_split(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uint64_t n, int nf, uint64_t *folds) {
+    if (!mt_key || !mt_pos || (n && (!colors || !folds)) || nf < 1) return fail(KP_E_ARG, "bad arguments");
+    if (*mt_pos < 0 || *mt_pos > 624) return fail(KP_E_ARG, "MT19937 position out of range");
+    kpf::mt19937 rng;
+    memcpy(rng.key, mt_key, sizeof(rng.key));
+    rng.pos = *mt_pos;
+    std::vector<uint64_t> col(colors, colors + n), tail(n), s(n);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += col[i];
+    const uint64_t per_fold = total / (uint64_t)nf;  // n_samples = n // n_folds (CV_tools.py:51)
+    for (int f = 0; f + 1 < nf; ++f) {
+        uint64_t acc = 0;
+        for (uint64_t i = n; i-- > 0;) {
+            acc += col[i];
+            tail[i] = acc;
+        }
+        kpf::sample(rng, per_fold, col.data(), tail.data(), n, s.data());
+        for (uint64_t i = 0; i < n; ++i) {
+            folds[i * (uint64_t)nf + f] = s[i];
+            col[i] -= s[i];
+        }
+    }
+    for (uint64_t i = 0; i < n; ++i) folds[i * (uint64_t)nf + (nf - 1)] = col[i];
+    memcpy(mt_key, rng.key, sizeof(rng.key));
+    *mt_pos = rng.pos;
     return KP_OK;
 }
 

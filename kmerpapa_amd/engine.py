@@ -58,7 +58,7 @@ class KPPassStats(ctypes.Structure):
 
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
            "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_pass", "kp_last_pass_stats",
-           "kp_fit_leaves", "kp_dump_lane"]
+           "kp_fit_leaves", "kp_dump_lane", "kp_fold_split"]
 
 
 def load():
@@ -88,6 +88,7 @@ def load():
         L.kp_last_pass_stats.argtypes = [vp, ctypes.POINTER(KPPassStats)]
         L.kp_fit_leaves.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u64p]
         L.kp_dump_lane.argtypes = [vp, ctypes.c_uint32, vp, vp]
+        L.kp_fold_split.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_int, vp]
         for name in EXPORTS:
             if name not in ("kp_destroy", "kp_plan_destroy", "kp_last_error"):
                 getattr(L, name).restype = ctypes.c_int
@@ -114,6 +115,24 @@ def kernel_tag():
             with open(os.path.join(src, name), "rb") as f:
                 h.update(name.encode() + b"\0" + f.read())
     return h.hexdigest()[:12]
+
+
+def fold_split(colors, n_folds, prng):
+    """Fold split of ``colors`` with the caller's numpy ``RandomState`` stream, in C++
+    (``kp_fold_split``; bit-identical to CV_tools.py:5-62).  ``prng`` is advanced exactly
+    as numpy's own draws would advance it.  Returns uint64 ``[n, n_folds]``."""
+    L = load()
+    st = prng.get_state(legacy=True)
+    if st[0] != "MT19937":
+        raise ValueError("fold split needs a legacy MT19937 RandomState")
+    key = np.array(st[1], dtype=np.uint32)
+    pos = ctypes.c_int32(int(st[2]))
+    col = np.ascontiguousarray(colors, dtype=np.uint64)
+    out = np.zeros((col.shape[0], int(n_folds)), dtype=np.uint64)
+    _check(L.kp_fold_split(_ptr(key), ctypes.byref(pos), _ptr(col), ctypes.c_uint64(col.shape[0]), int(n_folds),
+                           _ptr(out)))
+    prng.set_state((st[0], key, pos.value, st[3], st[4]))
+    return out
 
 
 def device_count():

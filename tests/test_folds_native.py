@@ -1,0 +1,55 @@
+"""The C++ fold split (kp_fold_split, kmerpapa_amd/csrc/kp_folds.h) against numpy itself:
+same folds and the same final MT19937 state as the reference's colour-by-colour
+RandomState.hypergeometric walk (CV_tools.py:5-62), for small and huge counts, zero
+colours, HYP (sample <= 10) and HRUA draws.  Host code: no GPU needed."""
+import numpy as np
+import pytest
+
+from kmerpapa_amd import engine
+from kmerpapa_amd.CV_tools import _split_colors_numpy
+
+
+def _pair(colors, nf, seed, itype=np.uint64):
+    p1, p2 = np.random.RandomState(seed), np.random.RandomState(seed)
+    a = _split_colors_numpy(np.asarray(colors, dtype=itype), nf, itype, p1)
+    b = engine.fold_split(np.asarray(colors, dtype=itype), nf, p2)
+    s1, s2 = p1.get_state(), p2.get_state()
+    return a, b, s1, s2
+
+
+@pytest.mark.parametrize("kind", range(5))
+def test_fold_split_matches_numpy_stream(kind):
+    rng = np.random.RandomState(100 + kind)
+    for trial in range(60):
+        n = int(rng.randint(1, 80))
+        if kind == 0:
+            colors = rng.randint(0, 12, size=n)            # mostly HYP draws
+        elif kind == 1:
+            colors = rng.randint(0, 5000, size=n)
+        elif kind == 2:
+            colors = rng.randint(0, 2 ** 31, size=n) // (1 + rng.randint(0, 1000, size=n))
+        elif kind == 3:
+            colors = np.where(rng.rand(n) < 0.4, 0, rng.randint(0, 10 ** 7, size=n))
+        else:
+            colors = rng.randint(0, 2 ** 33, size=n)      # > 2^32 totals (uint64 itype)
+        nf = int(rng.randint(1, 8))
+        a, b, s1, s2 = _pair(colors, nf, int(rng.randint(0, 2 ** 31)))
+        assert np.array_equal(a, b), (kind, trial)
+        assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2], "RandomState advanced differently"
+
+
+def test_fold_split_edge_cases():
+    for colors in ([0], [5], [0, 0, 0], [1, 0, 0, 7], [10 ** 9, 1]):
+        for nf in (1, 2, 5):
+            a, b, s1, s2 = _pair(colors, nf, 3)
+            assert np.array_equal(a, b)
+            assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]
+
+
+def test_fold_split_continues_the_callers_stream():
+    """Two successive splits on one RandomState (CV iterations) stay in lock step."""
+    colors = np.random.RandomState(1).randint(0, 3000, size=500).astype(np.uint64)
+    p1, p2 = np.random.RandomState(9), np.random.RandomState(9)
+    for _ in range(3):
+        assert np.array_equal(_split_colors_numpy(colors, 4, np.uint64, p1), engine.fold_split(colors, 4, p2))
+    assert p1.randint(0, 2 ** 30) == p2.randint(0, 2 ** 30)
