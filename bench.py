@@ -129,9 +129,11 @@ def committed_traffic(gen_pat, n_lanes, kernel_tag):
 def full_cv(plan, prep, rank, world):
     """The whole 5x5 grid x 5 folds as the CV driver runs it: this rank's share of the
     (alpha, fold) groups, one pass each, root read-out included."""
+    from kmerpapa_amd.engine import pack_passes
+    from kmerpapa_amd.shard import rank_groups
     t0 = time.perf_counter()
-    mine = prep["groups"][rank::world]
-    roots = [plan.run([g]) for g in mine]
+    mine = rank_groups(prep["groups"], rank, world)  # lane-granular share (15-16 lanes at N=8)
+    roots = [plan.run(p) for p in pack_passes(mine, min(plan.lanes_that_fit(), 8))]
     return time.perf_counter() - t0, len(mine), roots
 
 

@@ -1,0 +1,257 @@
+// kp_dp_kernel.h -- the lattice-DP sweep kernel (value-only), included by kp_hip.hip.
+//
+// Kept in its own file so that profiles can be tied to the exact sweep source: the
+// kernel tag bench.py records (engine.kernel_tag) hashes kp_core.h, kp_plan.h and this
+// file only.  See kp_hip.hip's header for the phases.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kp_core.h"
+
+#define KP_DP_MAX_THREADS 1024
+
+// LDS-qualified element types: pointers to them are 32-bit and address LDS directly
+typedef __attribute__((address_space(3))) float kp_lds_f32;
+typedef __attribute__((address_space(3))) uint64_t kp_lds_u64;
+
+struct kp_dev_tables {
+    const kp_postab *tabs;
+    const uint32_t *lowinfo;
+    const int32_t *loff;
+    const uint32_t *klofs;
+    const uint16_t *kllist;
+    const uint32_t *hlist;
+    const kp_lowdesc *ldesc;
+    const uint64_t *pw;
+    const uint64_t *hdig;
+    const uint8_t *lowmask;
+};
+
+struct kp_dp_params {
+    kp_geom g;
+    kp_dev_tables T;
+    const void *K;
+    float *S;
+    const kp_group_dev *groups;
+    uint64_t hbase;
+    int H;
+    int lmax;
+    uint32_t ptab_entries;     // separable count table entries (kp_plan.h)
+    uint32_t pscratch_entries; // largest intermediate table of its build
+    int remap;  // 1 = XCD-contiguous block order (KP_XCD_REMAP=1; measured 4% slower, off by default)
+    unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
+    int dbg;  // timing ablation only (KP_DEBUG_SKIP, wrong results): 1 = skip gather, 2 = skip level phase,
+              // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier
+};
+
+#ifdef KP_STAMPS
+// diagnostic build: lane 0 of every workgroup sums the shader-clock ticks of each phase
+// in LDS and flushes them with one global atomic per slot at the end (never read by the
+// kernel; outputs are unchanged)
+#define KP_STAMP(slot)                                                                        \
+    do {                                                                                      \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                           \
+        if (threadIdx.x == 0) st_lds[slot] += t_ - st_prev;                                   \
+        st_prev = t_;                                                                         \
+    } while (0)
+#else
+#define KP_STAMP(slot) \
+    do {               \
+    } while (0)
+#endif
+
+#define KP_IPT 2  // low cells per thread per level (host checks level sizes)
+
+// float4 min-update with a split candidate a + b (fminf drops NaN candidates like "<")
+__device__ inline void kp_min4v(float4 &best, const float4 a, const float4 b) {
+    best.x = fminf(best.x, a.x + b.x);
+    best.y = fminf(best.y, a.y + b.y);
+    best.z = fminf(best.z, a.z + b.z);
+    best.w = fminf(best.w, a.w + b.w);
+}
+
+template <typename CT, int NL>
+__global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const kp_geom &g = P.g;
+#ifdef KP_STAMPS
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+    const unsigned long long st_real0 = __builtin_amdgcn_s_memrealtime(), st_t0 = st_prev;
+#endif
+    uint32_t widx = blockIdx.x;
+    if (P.remap) {  // XCD-contiguous runs of the level's block list (A/B option)
+        const uint32_t nb = gridDim.x, q = nb >> 3, r = nb & 7u, x = blockIdx.x & 7u;
+        widx = x * q + (x < r ? x : r) + (blockIdx.x >> 3);
+    }
+    const uint64_t h = P.T.hlist[P.hbase + widx];
+    const kp_group_dev *G = P.groups + blockIdx.y;
+    const uint32_t lane0 = (uint32_t)G->lane0;
+    const int fold = G->fold;
+    const double alpha = G->alpha, beta = G->beta;
+    const uint32_t Bpad = g.Bpad;
+    double pen[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
+
+    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | pw[t][16] | lm[t][16]
+    //      (count-table scratch aliases st, which the gather fills afterwards; every carve
+    //       offset is a multiple of 16 bytes)
+    const size_t st_bytes = (size_t)NL * Bpad * 4, scr_bytes = (size_t)P.pscratch_entries * 4 * sizeof(CT);
+    float *st = reinterpret_cast<float *>(smem);
+    CT *ptab = reinterpret_cast<CT *>(smem + (st_bytes > scr_bytes ? st_bytes : ((scr_bytes + 15) & ~(size_t)15)));
+    kp_hpair *hp = reinterpret_cast<kp_hpair *>(ptab + (((size_t)P.ptab_entries * 2 + 3) & ~(size_t)3));
+    uint64_t *pw = reinterpret_cast<uint64_t *>(hp + (g.kh * 7 + 1));
+    uint8_t *lm = reinterpret_cast<uint8_t *>(pw + g.t * 16);
+#ifdef KP_STAMPS
+    unsigned long long *st_lds = reinterpret_cast<unsigned long long *>(lm + ((g.t * 16 + 15) & ~15));
+    if (threadIdx.x < 32) st_lds[threadIdx.x] = 0;
+#endif
+
+    const CT *K = reinterpret_cast<const CT *>(P.K);
+    // the block's high split pairs, scan order (kp_high_pairs): digits come packed from the
+    // plan (no 64-bit division), counts per position are uniform loads, and wave 0 writes
+    // one pair per lane
+    const uint64_t hd = P.T.hdig[P.hbase + widx];
+    int np = 0;
+    if (!(P.dbg & 1))
+        for (int i = 0; i < g.kh; ++i) np += P.T.tabs[g.t + i].np[(hd >> (4 * i)) & 15u];
+    const uint64_t rowstride = (uint64_t)g.Ltot * Bpad;
+    for (int p = (int)threadIdx.x; threadIdx.x < 64 && p < np; p += 64) {  // wave 0
+        int rem = p, i = 0;
+        uint32_t d = 0;
+        for (; i < g.kh; ++i) {
+            d = (uint32_t)(hd >> (4 * i)) & 15u;
+            const int npi = P.T.tabs[g.t + i].np[d];
+            if (rem < npi) break;
+            rem -= npi;
+        }
+        const kp_postab &T = P.T.tabs[g.t + i];
+        hp[p].h1 = (h - (uint64_t)(d - T.pa[d][rem]) * g.hcg[i]) * rowstride;  // child rows as element
+        hp[p].h2 = (h - (uint64_t)(d - T.pb[d][rem]) * g.hcg[i]) * rowstride;  // offsets of lane 0
+        hp[p].code = (uint32_t)(((g.t + i) << 3) | rem);
+    }
+    for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 32u; e += blockDim.x)
+        reinterpret_cast<uint32_t *>(pw)[e] = reinterpret_cast<const uint32_t *>(P.T.pw)[e];
+    for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 16u; e += blockDim.x) lm[e] = P.T.lowmask[e];
+    __syncthreads();  // lm is read by every thread below
+
+    // ---- separable count tables (train counts of the group fold), kp_core.h ----
+    kp_build_count_table<CT>(g, K, h, fold, lm, reinterpret_cast<CT *>(smem),
+                             reinterpret_cast<CT *>(smem) + (size_t)P.pscratch_entries * 2, ptab, threadIdx.x,
+                             blockDim.x, [] { __syncthreads(); });
+    __syncthreads();
+    KP_STAMP(0);
+
+    // ---- gather: high-position splits, as whole child-block rows (value only) ----
+    const uint32_t nch = Bpad / 4;
+    for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
+        const uint32_t ll = item / nch, c = item % nch;
+        const uint64_t lrow = (uint64_t)(lane0 + ll) * Bpad + 4 * c;
+        const float *base = P.S + lrow;
+        float4 best = make_float4(__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf(),
+                                  __builtin_huge_valf());
+        int p = 0;
+        for (; p + 4 <= np; p += 4) {
+            const float4 a0 = *reinterpret_cast<const float4 *>(base + hp[p].h1);
+            const float4 b0 = *reinterpret_cast<const float4 *>(base + hp[p].h2);
+            const float4 a1 = *reinterpret_cast<const float4 *>(base + hp[p + 1].h1);
+            const float4 b1 = *reinterpret_cast<const float4 *>(base + hp[p + 1].h2);
+            const float4 a2 = *reinterpret_cast<const float4 *>(base + hp[p + 2].h1);
+            const float4 b2 = *reinterpret_cast<const float4 *>(base + hp[p + 2].h2);
+            const float4 a3 = *reinterpret_cast<const float4 *>(base + hp[p + 3].h1);
+            const float4 b3 = *reinterpret_cast<const float4 *>(base + hp[p + 3].h2);
+            kp_min4v(best, a0, b0);
+            kp_min4v(best, a1, b1);
+            kp_min4v(best, a2, b2);
+            kp_min4v(best, a3, b3);
+        }
+        for (; p < np; ++p) {
+            const float4 a0 = *reinterpret_cast<const float4 *>(base + hp[p].h1);
+            const float4 b0 = *reinterpret_cast<const float4 *>(base + hp[p].h2);
+            kp_min4v(best, a0, b0);
+        }
+        float *sl = st + (size_t)(4 * c) * NL + ll;
+        sl[0] = best.x;
+        sl[NL] = best.y;
+        sl[2 * NL] = best.z;
+        sl[3 * NL] = best.w;
+    }
+    __syncthreads();
+    KP_STAMP(1);
+
+    // ---- levels: low cells inside the block, level by level ----
+    // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
+    // the next level's descriptors are loaded while the current level computes
+    const bool high_zero = (P.H == 0);
+    const int lmax = (P.dbg & 2) ? -1 : P.lmax;
+    const uint4 *desc = reinterpret_cast<const uint4 *>(P.T.ldesc);
+    uint4 cur[KP_IPT], nxt[KP_IPT];
+    {
+        const int beg = P.T.loff[0], cnt = P.T.loff[1] - beg;
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) {
+            const int q = (int)threadIdx.x + k * (int)blockDim.x;
+            if (q < cnt) cur[k] = desc[beg + q];
+        }
+    }
+    for (int lam = 0; lam <= lmax; ++lam) {
+        const int beg = P.T.loff[lam], cnt = P.T.loff[lam + 1] - beg;
+        if (lam < lmax) {
+            const int nbeg = P.T.loff[lam + 1], ncnt = P.T.loff[lam + 2] - nbeg;
+#pragma unroll
+            for (int k = 0; k < KP_IPT; ++k) {
+                const int q = (int)threadIdx.x + k * (int)blockDim.x;
+                if (q < ncnt) nxt[k] = desc[nbeg + q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) {
+            const int q = (int)threadIdx.x + k * (int)blockDim.x;
+            if (q < cnt) {
+                const uint32_t l = cur[k].x & 0xFFFFu;
+                const uint32_t info = cur[k].z;
+                // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
+                kp_single_ctx sc;
+                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
+                sc.kmer = high_zero && lam == 0;
+                sc.c.mte = sc.c.ute = 0;
+                sc.logp = sc.log1mp = 0.0;
+                if (!sc.kmer && !(P.dbg & 4)) {
+                    const double pr = kp_rate(sc.c, alpha, beta);
+                    sc.logp = log(pr);
+                    sc.log1mp = log(1.0 - pr);
+                }
+                if (!(P.dbg & 8)) {
+                    kp_dp_cell_values<NL>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta, pen);
+                } else {  // timing ablation: no split scan, keep the single term
+#pragma unroll
+                    for (int j = 0; j < NL; ++j)
+                        st[l * NL + j] = (float)kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
+                }
+            }
+        }
+        if (!(P.dbg & 16)) __syncthreads();  // (ablation 16: timing without the level barrier)
+        KP_STAMP(3 + lam);
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) cur[k] = nxt[k];
+    }
+
+    // ---- store the block's score rows ----
+    for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
+        const uint32_t ll = item / nch, c = item % nch;
+        const float *sl = st + (size_t)(4 * c) * NL + ll;
+        *reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c) =
+            make_float4(sl[0], sl[NL], sl[2 * NL], sl[3 * NL]);
+    }
+    KP_STAMP(2);
+#ifdef KP_STAMPS
+    if (threadIdx.x == 0 && P.stamps) {
+        for (int q = 0; q < 30; ++q)
+            if (st_lds[q]) atomicAdd(P.stamps + q, st_lds[q]);
+        atomicAdd(P.stamps + 30, __builtin_amdgcn_s_memtime() - st_t0);
+        atomicAdd(P.stamps + 31, __builtin_amdgcn_s_memrealtime() - st_real0);
+    }
+#endif
+}
+

@@ -106,12 +106,13 @@ def _ptr(a):
 
 
 def kernel_tag():
-    """Short hash of the HIP sources the library was built from (ties profiles to a build)."""
+    """Short hash of the sweep kernel's sources (kp_core.h, kp_dp_kernel.h, kp_plan.h):
+    ties PMC profiles to the kernel build they measured."""
     import hashlib
     h = hashlib.sha1()
     src = os.path.join(_HERE, "csrc")
-    for name in sorted(os.listdir(src)):
-        if name.endswith((".hip", ".h")):
+    for name in ("kp_core.h", "kp_dp_kernel.h", "kp_plan.h"):
+        if True:
             with open(os.path.join(src, name), "rb") as f:
                 h.update(name.encode() + b"\0" + f.read())
     return h.hexdigest()[:12]

@@ -29,9 +29,21 @@ def chunk_bounds(lane_counts, parts):
 
 
 def rank_groups(groups, rank, world):
-    """This rank's contiguous chunk of ``groups`` (list of (fold, alpha, beta, penalties))."""
-    b = chunk_bounds([len(g[3]) for g in groups], world)
-    return groups[b[rank]:b[rank + 1]]
+    """This rank's share of ``groups`` (list of (fold, alpha, beta, penalties)), split at
+    LANE granularity: the lanes (one penalty of one group) in group-major order are cut into
+    ``world`` contiguous runs of equal length, and each run is regrouped by (fold, alpha).
+    125 lanes of a 5x5x5 grid over 8 GPUs give every rank 15-16 lanes instead of 3-4
+    whole groups.  Concatenating the ranks' lanes in rank order gives the original order."""
+    lanes = [(g[0], g[1], g[2], c, gi) for gi, g in enumerate(groups) for c in g[3]]
+    n = len(lanes)
+    lo, hi = (n * rank) // world, (n * (rank + 1)) // world
+    out = []
+    for fold, alpha, beta, c, gi in lanes[lo:hi]:
+        if out and out[-1][4] == gi:
+            out[-1][3].append(c)
+        else:
+            out.append([fold, alpha, beta, [c], gi])
+    return [(f, a, b, pens) for f, a, b, pens, _ in out]
 
 
 def sharded_run_groups(run_groups, rank, world, all_gather, devices=None):

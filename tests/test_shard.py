@@ -11,6 +11,17 @@ from kmerpapa_amd import shard
 from tests.fixtures import golden_json
 
 
+def test_rank_groups_split_lanes_evenly_in_order():
+    groups = [(f, a, 0.1 * f + a, [3.0, 4.0, 5.0, 6.0, 7.0]) for a in (0.5, 1.0, 2.0, 5.0, 10.0) for f in range(5)]
+    flat = [(g[0], g[1], c) for g in groups for c in g[3]]
+    for world in (1, 2, 3, 4, 8):
+        parts = [shard.rank_groups(groups, r, world) for r in range(world)]
+        got = [(g[0], g[1], c) for p in parts for g in p for c in g[3]]
+        assert got == flat
+        sizes = [sum(len(g[3]) for g in p) for p in parts]
+        assert max(sizes) - min(sizes) <= 1
+
+
 def test_chunk_bounds_cover_every_group_once():
     for n in range(0, 30):
         lanes = [1 + (i * 7) % 5 for i in range(n)]
@@ -49,7 +60,7 @@ def _work(rank, world, q):
         ran = []
 
         def counting(gen_pat, M, U, groups, devices=None, max_block=0):
-            ran.extend((g[0], g[1], tuple(g[3])) for g in groups)
+            ran.extend((g[0], g[1], c) for g in groups for c in g[3])
             return E.run_groups(gen_pat, M, U, groups, devices=devices, max_block=max_block)
         run = shard.sharded_run_groups(counting, rank, world, shard.torch_all_gather())
         res = cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], 1, np.uint32,
@@ -80,6 +91,6 @@ def test_two_rank_gloo_cv_matches_single_process():
         assert tr is not None, f"rank {rank} failed: {te}"
         assert tr == ref["train"].tobytes() and te == ref["test"].tobytes(), f"rank {rank} roots differ"
         ran_all.extend(ran)
-    want = [(f, a, tuple(c["penalties"])) for a in c["alphas"] for f in range(c["nfolds"])]
-    assert sorted(ran_all) == sorted(want)  # every (alpha, fold) group exactly once over both ranks
+    want = [(f, a, p) for a in c["alphas"] for f in range(c["nfolds"]) for p in c["penalties"]]
+    assert sorted(ran_all) == sorted(want)  # every lane (alpha, fold, penalty) exactly once over both ranks
     assert all(len(r) > 0 for _, _, _, r in outs)  # both ranks did work
