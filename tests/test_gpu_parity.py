@@ -179,16 +179,43 @@ def test_fit7_partition(eng):
     assert names == fo["names"]
 
 
-def test_cv7_roots(eng):
-    g = golden_json("cv7.json")
-    if g is None:
-        pytest.skip("7-mer CV golden not generated")
+def test_cv7_roots_vs_oracle(eng):
+    """7-mer test data (34,171,875 cells), 5-fold CV through the drop-in driver: every
+    fold's root train/test value equals the oracle's (pinned to the reference), bit for
+    bit.  (The reference itself needs hours per pass here, so the oracle is the checker.)"""
     from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    from kmerpapa_amd.CV_tools import fold_tables
+    from oracle import oracle as O
     ctx, gp, nm, nu = context_table(7)
-    res = cvm.cv_roots(gp, ctx, g["alphas"], g["penalties"], 5, 1, 1, np.uint32, devices=[0])
-    ps = g["passes"][0]
-    assert bits_equal(res["test"][0, 0, 0], np.array(ps["root_test"], np.float32))
-    assert bits_equal(res["train"][0, 0, 0], np.array(ps["root_train"], np.float32))
+    alphas, pens = [1.0], [5.0, 3.0]
+    res = cvm.cv_roots(gp, ctx, alphas, pens, 5, 1, 1, np.uint32, devices=[0])
+    contexts, Mf, Uf = fold_tables(ctx, 5, np.random.RandomState(1), np.uint32)
+    ref = O.cv_pass(gp, contexts, Mf, Uf, alphas[0], res["betas"][0, 0], pens[0], 32)
+    assert bits_equal(res["train"][0, 0, 0], ref["root_train"])
+    assert bits_equal(res["test"][0, 0, 0], ref["root_test"])
+
+
+def test_9mer_sublattice_fit_vs_oracle(eng):
+    """Synthetic 9-mer counts of the benchmark restricted to ANNNMNNNA (34M cells): the fit
+    (score, M, U, partition in backtrack order) equals the oracle's."""
+    import bench
+    from kmerpapa_amd.algorithms import bottum_up_array_w_numba as fitm
+    from oracle import oracle as O
+    kmers, M, U = bench.synthetic_counts("ANNNMNNNA", seed=9)
+    ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
+    nm, nu = int(M.sum()), int(U.sum())
+    my = nm / (nm + nu)
+    alpha, pen = 1.0, 4.0
+    beta = (alpha * (1.0 - my)) / my
+
+    class A:
+        verbosity = 0
+    sc, Mr, Ur, names = fitm.pattern_partition_bottom_up("ANNNMNNNA", ctx, alpha, beta, pen, A, nm, nu)
+    rs, rm, ru, rnames, _ = O.fit("ANNNMNNNA", list(ctx), M, U, alpha, beta, pen, 32)
+    assert np.float32(sc).tobytes() == np.float32(rs).tobytes()
+    assert (int(Mr), int(Ur)) == (rm, ru)
+    assert names == rnames
+    assert len(names) > 50
 
 
 def _random_case(rng, k):
