@@ -44,6 +44,14 @@ ALPHAS = [0.5, 1.0, 2.0, 5.0, 10.0]
 PENALTIES = [3.0, 4.0, 5.0, 6.0, 7.0]
 NFOLDS = 5
 PEAK_HBM_GBS = 8000.0
+# BASELINE.json configs[4]: synthetic 11-mers, 7x7 grid, 10-fold CV.  The all-N 11-mer
+# lattice (1.7e12 cells) needs >= 41 TB per lane, so -- as SURVEY.md 8(d) prescribes -- the
+# flanks are fixed by a super-pattern: ANNNNMNNNNA has the 9-mer's 7.69e9 cells.
+CONFIGS = {
+    "9mer": dict(gen_pat="NNNNMNNNN", alphas=ALPHAS, penalties=PENALTIES, nfolds=5),
+    "11mer": dict(gen_pat="ANNNNMNNNNA", alphas=[0.5, 1.0, 2.0, 3.0, 5.0, 7.0, 10.0],
+                  penalties=[2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0], nfolds=10),
+}
 
 
 def synthetic_counts(gen_pat=GEN_PAT, seed=9):
@@ -66,49 +74,55 @@ def synthetic_counts(gen_pat=GEN_PAT, seed=9):
     return kmers, pos.astype(np.int64), (bg - pos).astype(np.int64)
 
 
-def prepare(gen_pat, seed=1):
+def prepare(gen_pat, seed=1, alphas=ALPHAS, penalties=PENALTIES, nfolds=NFOLDS):
     """Fold split (reference RNG stream) and betas for every (alpha, fold)."""
     kmers, M, U = synthetic_counts(gen_pat)
     ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
     total = int(M.sum() + U.sum())
     itype = np.uint64 if total > np.iinfo(np.uint32).max else np.uint32
     t0 = time.time()
-    contexts, Mf, Uf = fold_tables(ctx, NFOLDS, np.random.RandomState(seed), itype)
+    contexts, Mf, Uf = fold_tables(ctx, nfolds, np.random.RandomState(seed), itype)
     t_fold = time.time() - t0
     Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, generality(gen_pat), itype)
     msum = Mk.sum(axis=0, dtype=np.uint64)
     usum = Uk.sum(axis=0, dtype=np.uint64)
     mtr, utr = msum.sum() - msum, usum.sum() - usum
     groups = []
-    for a in ALPHAS:
+    for a in alphas:
         my = mtr / (mtr + utr)
         betas = (a * (1.0 - my)) / my
-        for f in range(NFOLDS):
-            groups.append((f, a, float(betas[f]), list(PENALTIES)))
+        for f in range(nfolds):
+            groups.append((f, a, float(betas[f]), list(penalties)))
     return {"Mk": Mk, "Uk": Uk, "groups": groups, "itype": itype, "t_fold_s": t_fold, "contexts": contexts,
-            "Mf": Mf, "Uf": Uf, "total": total, "gen_pat": gen_pat}
+            "Mf": Mf, "Uf": Uf, "total": total, "gen_pat": gen_pat, "alphas": list(alphas),
+            "penalties": list(penalties), "nfolds": nfolds}
 
 
 def cpu_baseline(prep, seconds_hint=15.0):
     """Time the single-threaded CPU oracle on a bounded sample of the same counts: the
-    sub-lattice with both outermost positions fixed to 'A' (NNNMNNN-sized, 3.4e7 cells),
-    one (alpha, c) over all 5 folds."""
+    sub-lattice with the two outermost ambiguous positions fixed to 'A' (3.4e7 cells),
+    one (alpha, c) over all folds."""
     from oracle import oracle as O
-    sub = "A" + prep["gen_pat"][1:-1] + "A"
-    keep = [i for i, c in enumerate(prep["contexts"]) if c[0] == "A" and c[-1] == "A"]
+    gp = prep["gen_pat"]
+    # fix the two outermost still-ambiguous positions to A: a 15^6 x 3 = 3.4e7-cell sample
+    amb = [i for i, x in enumerate(gp) if x != "A"]
+    fixed = {amb[0], amb[-1]}
+    sub = "".join("A" if i in fixed else x for i, x in enumerate(gp))
+    keep = [j for j, c in enumerate(prep["contexts"]) if all(c[i] == "A" for i in fixed)]
     ctxs = [prep["contexts"][i] for i in keep]
     Mf = prep["Mf"][keep]
     Uf = prep["Uf"][keep]
     g = prep["groups"][0]
-    betas = [prep["groups"][f][2] for f in range(NFOLDS)]
+    nf = prep["nfolds"]
+    betas = [prep["groups"][f][2] for f in range(nf)]
     bits = 8 * np.dtype(prep["itype"]).itemsize
     t0 = time.time()
     O.cv_pass(sub, ctxs, Mf, Uf, g[1], betas, g[3][0], bits)
     dt = time.time() - t0
-    units = O.npat(sub) * NFOLDS
+    units = O.npat(sub) * nf
     return {"value": units / dt, "unit": "cells*folds*(alpha,c)/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/kp_oracle.c kpo_cv on sub-lattice {sub} of the same 9-mer counts "
-                      f"({O.npat(sub)} cells x {NFOLDS} folds, 1 (alpha,c)) in {dt:.1f} s on 1 host core"}
+            "sample": f"oracle/kp_oracle.c kpo_cv on sub-lattice {sub} of the same counts "
+                      f"({O.npat(sub)} cells x {nf} folds, 1 (alpha,c)) in {dt:.1f} s on 1 host core"}
 
 
 def committed_traffic(gen_pat, n_lanes, kernel_tag):
@@ -142,7 +156,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--pattern", default=GEN_PAT)
+    ap.add_argument("--config", default="9mer", choices=sorted(CONFIGS),
+                    help="9mer = BASELINE configs[3] (the headline); 11mer = configs[4] (super-pattern restricted)")
+    ap.add_argument("--pattern", default=None, help="override the config's general pattern")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--max-block", type=int, default=0)
     ap.add_argument("--no-full-cv", action="store_true", help="skip the full 5x5x5 CV wall-clock leg")
@@ -156,8 +172,11 @@ def main():
         import torch.distributed as dist  # host-side barrier / max only (no data-path collective)
         dist.init_process_group("gloo")
 
-    gen_pat = a.pattern
-    prep = prepare(gen_pat)
+    cfg = dict(CONFIGS[a.config])
+    if a.pattern:
+        cfg["gen_pat"] = a.pattern
+    gen_pat = cfg["gen_pat"]
+    prep = prepare(gen_pat, alphas=cfg["alphas"], penalties=cfg["penalties"], nfolds=cfg["nfolds"])
     dev = engine.get_device(local)
     t0 = time.time()
     plan = engine.Plan(dev, gen_pat, a.max_block)
@@ -214,7 +233,8 @@ def main():
         ms_step = elapsed / a.steps * 1e3
         passes_full_cv = math.ceil(len(groups) / world)
         line = {
-            "metric": "patterns scored/sec (lattice cells x folds x (alpha,c)), 9-mer 5-fold CV 5x5 grid",
+            "metric": "patterns scored/sec (lattice cells x folds x (alpha,c)), 9-mer 5-fold CV 5x5 grid"
+                      if a.config == "9mer" else f"patterns scored/sec, {a.config} config",
             "value": units / elapsed,
             "unit": "cell-scores/s",
             "n_gpus": world,
@@ -226,12 +246,13 @@ def main():
             "vs_baseline": None,
             "dtype": "f32 (scores, split sums) + f64 (single-pattern term); u32 counts",
             "data": "synthetic",
-            "config": {"workload": f"synthetic 9-mer counts, general pattern {gen_pat} "
-                                   f"({plan.info['npat']} cells), 5x5 (alpha, c) grid, {NFOLDS}-fold CV; step = "
-                                   f"one (alpha, fold) group x {lanes} penalties over the whole lattice",
-                       "gen_pat": gen_pat, "cells": plan.info["npat"], "lanes_per_step": lanes,
+            "config": {"workload": f"synthetic {len(gen_pat)}-mer counts, general pattern {gen_pat} "
+                                   f"({plan.info['npat']} cells), {len(prep['alphas'])}x{len(prep['penalties'])} "
+                                   f"(alpha, c) grid, {prep['nfolds']}-fold CV; step = one (alpha, fold) group x "
+                                   f"{lanes} penalties over the whole lattice",
+                       "name": a.config, "gen_pat": gen_pat, "cells": plan.info["npat"], "lanes_per_step": lanes,
                        "units_per_step": plan.info["npat"] * lanes, "block_cells": plan.info["block"],
-                       "alphas": ALPHAS, "penalties": PENALTIES, "nfolds": NFOLDS},
+                       "alphas": prep["alphas"], "penalties": prep["penalties"], "nfolds": prep["nfolds"]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS,
                          "traffic": (tr["hbm_bytes_per_pass"] if tr else None),
@@ -244,8 +265,8 @@ def main():
             "dp_kernel_launches_per_step": sum(s["dp_launches"] for s in stats) / a.steps,
             "dp_kernel_avg_launch_ms": dp_ms / max(1, sum(s["dp_launches"] for s in stats)),
             "backtrack_ms_per_step": sum(s["backtrack_ms"] for s in stats) / a.steps,
-            "cv_5x5x5_wall_s": cv_wall,
-            "cv_5x5x5_wall_s_estimate": prep["t_fold_s"] + t_setup + passes_full_cv * ms_step / 1e3,
+            "cv_full_grid_wall_s": cv_wall,
+            "cv_full_grid_wall_s_estimate": prep["t_fold_s"] + t_setup + passes_full_cv * ms_step / 1e3,
             "fold_split_s": prep["t_fold_s"],
             "setup_s": t_setup,
             "kernel_tag": tag,
