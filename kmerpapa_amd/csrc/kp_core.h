@@ -234,11 +234,11 @@ __host__ __device__ inline uint32_t kp_mul24(uint32_t a, uint32_t b) { return (a
 // fminf: it ignores NaN exactly as "v < best" does, and every score is >= +0 (no -0).
 // ---------------------------------------------------------------------------
 
-// min over NP split pairs of one low position, NL lanes; all 2*NP*NL LDS reads issue
-// before the first min (fully unrolled)
-template <int NL, int NP, typename SP>
-__host__ __device__ inline void kp_pairs_minv(SP st, uint32_t l, uint32_t cg, uint64_t w, float *lmin) {
-    float va[NP][NL], vb[NP][NL];
+// min over NP split pairs of one low position for W lanes starting at lane j0 (lane
+// stride NL); all 2*NP*W LDS reads issue before the first min (fully unrolled)
+template <int NL, int W, int NP, typename SP>
+__host__ __device__ inline void kp_pairs_minv(SP st, uint32_t l, uint32_t cg, uint64_t w, uint32_t j0, float *lmin) {
+    float va[NP][W], vb[NP][W];
     const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -246,33 +246,35 @@ __host__ __device__ inline void kp_pairs_minv(SP st, uint32_t l, uint32_t cg, ui
         const uint32_t l1 = l - kp_mul24(wp & 15u, cg);
         const uint32_t l2 = l - kp_mul24((wp >> 4) & 15u, cg);
 #pragma unroll
-        for (int j = 0; j < NL; ++j) {
-            va[p][j] = st[l1 * NL + j];
-            vb[p][j] = st[l2 * NL + j];
+        for (int j = 0; j < W; ++j) {
+            va[p][j] = st[l1 * NL + j0 + j];
+            vb[p][j] = st[l2 * NL + j0 + j];
         }
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p)
 #pragma unroll
-        for (int j = 0; j < NL; ++j) lmin[j] = fminf(lmin[j], va[p][j] + vb[p][j]);
+        for (int j = 0; j < W; ++j) lmin[j] = fminf(lmin[j], va[p][j] + vb[p][j]);
 }
 
-
-// one DP cell for NL lanes (lanes interleaved in LDS: st[cell * NL + lane]); st[l] holds
-// the best high-position split gathered from HBM.  pw = pair words [t][16].
-template <int NL, typename SP, typename WP>
+// one DP cell for lanes j0 .. j0+W-1 of the NL lanes interleaved in LDS
+// (st[cell * NL + lane]); st[l] holds the best high-position split gathered from HBM.
+// pw = pair words [t][16]; pen = the W penalties of those lanes.  W = NL is the normal
+// mode (one thread per cell); W = 1 splits a cell's lanes over threads when a level has
+// few cells (shorter dependent chains on the narrow top levels of a block).
+template <int NL, int W, typename SP, typename WP>
 __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint32_t l, uint32_t lowinfo, SP st,
                                                   const kp_single_ctx &sc, double alpha, double beta,
-                                                  const double *pen) {
-    SP row = st + l * NL;
+                                                  const double *pen, uint32_t j0 = 0) {
+    SP row = st + l * NL + j0;
     if (sc.kmer) {  // level 0 (CV :145-151 / Fit :106-114)
 #pragma unroll
-        for (int j = 0; j < NL; ++j) row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
+        for (int j = 0; j < W; ++j) row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
         return;
     }
-    float lmin[NL];
+    float lmin[W];
 #pragma unroll
-    for (int j = 0; j < NL; ++j) lmin[j] = row[j];
+    for (int j = 0; j < W; ++j) lmin[j] = row[j];
     uint64_t w[KP_MAXT];
 #pragma unroll
     for (int i = 0; i < KP_MAXT; ++i) w[i] = (i < g.t) ? pw[i * 16 + kp_low_digit(lowinfo, i)] : 0;
@@ -284,22 +286,23 @@ __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint3
         const uint32_t np = (uint32_t)(w[i] >> 56);
         const uint32_t cg = (uint32_t)g.cgl[i] & 0xFFFFu;  // low place values are < 2^16 (block <= 65535)
         if (np == 1) {
-            kp_pairs_minv<NL, 1>(st, l, cg, w[i], lmin);
+            kp_pairs_minv<NL, W, 1>(st, l, cg, w[i], j0, lmin);
         } else if (np == 3) {
-            kp_pairs_minv<NL, 3>(st, l, cg, w[i], lmin);
+            kp_pairs_minv<NL, W, 3>(st, l, cg, w[i], j0, lmin);
         } else if (np == 7) {
-            kp_pairs_minv<NL, 7>(st, l, cg, w[i], lmin);
+            kp_pairs_minv<NL, W, 7>(st, l, cg, w[i], j0, lmin);
         } else {
             for (uint32_t p = 0; p < np; ++p) {  // not produced by the IUPAC tables; kept general
                 const uint32_t l1 = l - (uint32_t)((w[i] >> (8 * p)) & 15u) * cg;
                 const uint32_t l2 = l - (uint32_t)((w[i] >> (8 * p + 4)) & 15u) * cg;
 #pragma unroll
-                for (int j = 0; j < NL; ++j) lmin[j] = fminf(lmin[j], st[l1 * NL + j] + st[l2 * NL + j]);
+                for (int j = 0; j < W; ++j)
+                    lmin[j] = fminf(lmin[j], st[l1 * NL + j0 + j] + st[l2 * NL + j0 + j]);
             }
         }
     }
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
+    for (int j = 0; j < W; ++j) {
         float best = lmin[j];
         const double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
         if (s < (double)best) best = (float)s;  // float64 compare against the float32 store (CV :71)

@@ -40,6 +40,7 @@ struct kp_dp_params {
     uint32_t ptab_entries;     // separable count table entries (kp_plan.h)
     uint32_t pscratch_entries; // largest intermediate table of its build
     int remap;  // 1 = XCD-contiguous block order (KP_XCD_REMAP=1; measured 4% slower, off by default)
+    int lanesplit;  // split a cell's lanes over threads on narrow levels (KP_LANE_SPLIT=0 disables)
     unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
     int dbg;  // timing ablation only (KP_DEBUG_SKIP, wrong results): 1 = skip gather, 2 = skip level phase,
               // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier
@@ -186,25 +187,58 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     const bool high_zero = (P.H == 0);
     const int lmax = (P.dbg & 2) ? -1 : P.lmax;
     const uint4 *desc = reinterpret_cast<const uint4 *>(P.T.ldesc);
+    // narrow levels (cells x lanes <= threads, e.g. the block's top levels) split each
+    // cell's lanes over NL threads: the same work with a 1/NL-long dependent chain
+    const int nthr = (int)blockDim.x;
+    auto lane_split = [&](int cells) { return P.lanesplit && cells * NL <= nthr; };
     uint4 cur[KP_IPT], nxt[KP_IPT];
     {
         const int beg = P.T.loff[0], cnt = P.T.loff[1] - beg;
+        if (lane_split(cnt)) {
+            if ((int)threadIdx.x / NL < cnt) cur[0] = desc[beg + (int)threadIdx.x / NL];
+        } else {
 #pragma unroll
-        for (int k = 0; k < KP_IPT; ++k) {
-            const int q = (int)threadIdx.x + k * (int)blockDim.x;
-            if (q < cnt) cur[k] = desc[beg + q];
+            for (int k = 0; k < KP_IPT; ++k) {
+                const int q = (int)threadIdx.x + k * nthr;
+                if (q < cnt) cur[k] = desc[beg + q];
+            }
         }
     }
     for (int lam = 0; lam <= lmax; ++lam) {
         const int beg = P.T.loff[lam], cnt = P.T.loff[lam + 1] - beg;
         if (lam < lmax) {
             const int nbeg = P.T.loff[lam + 1], ncnt = P.T.loff[lam + 2] - nbeg;
+            if (lane_split(ncnt)) {
+                if ((int)threadIdx.x / NL < ncnt) nxt[0] = desc[nbeg + (int)threadIdx.x / NL];
+            } else {
 #pragma unroll
-            for (int k = 0; k < KP_IPT; ++k) {
-                const int q = (int)threadIdx.x + k * (int)blockDim.x;
-                if (q < ncnt) nxt[k] = desc[nbeg + q];
+                for (int k = 0; k < KP_IPT; ++k) {
+                    const int q = (int)threadIdx.x + k * nthr;
+                    if (q < ncnt) nxt[k] = desc[nbeg + q];
+                }
             }
         }
+        if (lane_split(cnt)) {
+            const int q = (int)threadIdx.x / NL;
+            const uint32_t j = threadIdx.x % NL;
+            if (q < cnt && !(P.dbg & 8)) {
+                const uint32_t l = cur[0].x & 0xFFFFu;
+                const uint32_t info = cur[0].z;
+                kp_single_ctx sc;
+                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
+                sc.kmer = high_zero && lam == 0;
+                sc.c.mte = sc.c.ute = 0;
+                sc.logp = sc.log1mp = 0.0;
+                if (!sc.kmer) {
+                    const double pr = kp_rate(sc.c, alpha, beta);
+                    sc.logp = log(pr);
+                    sc.log1mp = log(1.0 - pr);
+                }
+                const double pj = G->pen[j];
+                kp_dp_cell_values<NL, 1>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta, &pj,
+                                         j);
+            }
+        } else
 #pragma unroll
         for (int k = 0; k < KP_IPT; ++k) {
             const int q = (int)threadIdx.x + k * (int)blockDim.x;
@@ -223,7 +257,8 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                     sc.log1mp = log(1.0 - pr);
                 }
                 if (!(P.dbg & 8)) {
-                    kp_dp_cell_values<NL>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta, pen);
+                    kp_dp_cell_values<NL, NL>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta,
+                                              pen);
                 } else {  // timing ablation: no split scan, keep the single term
 #pragma unroll
                     for (int j = 0; j < NL; ++j)

@@ -735,6 +735,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.pscratch_entries = hp.pscratch_entries;
     P.dbg = getenv("KP_DEBUG_SKIP") ? atoi(getenv("KP_DEBUG_SKIP")) : 0;
     P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 0;
+    P.lanesplit = getenv("KP_LANE_SPLIT") ? atoi(getenv("KP_LANE_SPLIT")) : 1;
     P.stamps = nullptr;
 #ifdef KP_STAMPS
     static unsigned long long *d_stamps = nullptr;

@@ -21,14 +21,14 @@ std::string g_err;
 void cell_values(int nl, const kp_geom &g, const uint64_t *pw, uint32_t l, uint32_t info, float *st,
                  const kp_single_ctx &sc, double a, double b, const double *pen) {
     switch (nl) {
-        case 1: kp_dp_cell_values<1>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 2: kp_dp_cell_values<2>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 3: kp_dp_cell_values<3>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 4: kp_dp_cell_values<4>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 5: kp_dp_cell_values<5>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 6: kp_dp_cell_values<6>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 7: kp_dp_cell_values<7>(g, pw, l, info, st, sc, a, b, pen); break;
-        default: kp_dp_cell_values<8>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 1: kp_dp_cell_values<1, 1>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 2: kp_dp_cell_values<2, 2>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 3: kp_dp_cell_values<3, 3>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 4: kp_dp_cell_values<4, 4>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 5: kp_dp_cell_values<5, 5>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 6: kp_dp_cell_values<6, 6>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 7: kp_dp_cell_values<7, 7>(g, pw, l, info, st, sc, a, b, pen); break;
+        default: kp_dp_cell_values<8, 8>(g, pw, l, info, st, sc, a, b, pen); break;
     }
 }
 
