@@ -1,0 +1,29 @@
+"""End-to-end CLI run on the benchmark's synthetic 9-mer counts (BASELINE configs[3]):
+writes positive/background count files, then times `python -m kmerpapa_amd` exactly as a
+user would run it (grid CV + final fit + output table).  Prints one JSON line."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "cli9")
+os.makedirs(out, exist_ok=True)
+kmers, M, U = bench.synthetic_counts("NNNNMNNNN")
+with open(os.path.join(out, "pos.txt"), "w") as f:
+    f.writelines(f"{k} {m}\n" for k, m in zip(kmers, M))
+with open(os.path.join(out, "bg.txt"), "w") as f:
+    f.writelines(f"{k} {m + u}\n" for k, m, u in zip(kmers, M, U))
+cmd = [sys.executable, "-m", "kmerpapa_amd", "-p", os.path.join(out, "pos.txt"), "-b", os.path.join(out, "bg.txt"),
+       "-c", "3", "4", "5", "6", "7", "-a", "0.5", "1", "2", "5", "10", "--nfolds", "5", "--seed", "1",
+       "-o", os.path.join(out, "partition.txt"), "-f", os.path.join(out, "cv.txt")]
+t0 = time.time()
+r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
+wall = time.time() - t0
+lines = open(os.path.join(out, "partition.txt")).read().splitlines() if r.returncode == 0 else []
+print(json.dumps({"cmd": " ".join(cmd[1:]), "rc": r.returncode, "wall_s": wall, "patterns": max(0, len(lines) - 1),
+                  "stderr_tail": r.stderr[-1500:]}))
