@@ -1,0 +1,70 @@
+"""One rate per k-mer, cross-validated over the pseudo count -- drop-in for the
+reference's ``kmerpapa.algorithms.all_kmers_CV`` (src/kmerpapa/algorithms/all_kmers_CV.py,
+v0.2.4; ``--score all_kmers``).
+
+There is no lattice DP here: every k-mer is its own pattern, so the per-k-mer test
+-2LL is a closed form.  The fold split is the shared one (CV_tools, native
+``kp_fold_split``); the loss is evaluated for all k-mers at once with numpy, keeping
+the reference's operation order and its sequential float64 accumulation over k-mers
+(``sum_test += ...`` in ``matches`` order, :36-41), so results are bit-identical.
+"""
+import sys
+
+import numpy as np
+from scipy.special import xlog1py, xlogy
+
+from ..CV_tools import make_all_folds_contextD_kmers
+from ..pattern_utils import generality
+from ..score_utils import get_betas
+
+
+def test_folds(trainM, trainU, testM, testU, alphas, betas):
+    """-2 LL of test counts under the training rate (ref :8-13)."""
+    p = (trainM + alphas) / (trainM + trainU + alphas + betas)
+    return -2 * (xlogy(testM, p) + xlog1py(testU, -p))
+
+
+def _seq_sum_rows(terms):
+    """Row-by-row float64 sum from 0.0, in order (what ``s += row`` does in a loop)."""
+    if terms.shape[0] == 0:
+        return np.zeros(terms.shape[1])
+    return np.add.accumulate(terms, axis=0)[-1] + 0.0
+
+
+def all_kmers(gen_pat, contextD, alphas, args, nmut, nunmut, index_mut=0):
+    """Best pseudo count for one-rate-per-k-mer (ref :15-63).  Returns ``(best_alpha, best_test_loss)``."""
+    nf = args.nfolds
+    nit = args.iterations
+    npat = generality(gen_pat)
+    U_mem = np.zeros((npat, nf), dtype=np.uint64)
+    M_mem = np.zeros((npat, nf), dtype=np.uint64)
+    test_loss = {a_i: [] for a_i in range(len(alphas))}
+    train_loss = {a_i: [] for a_i in range(len(alphas))}
+    if index_mut != 0:
+        contextD = {k: (v[index_mut], v[-1]) for k, v in contextD.items()}
+    prng = np.random.RandomState(args.seed)
+    for _ in range(nit):
+        make_all_folds_contextD_kmers(contextD, U_mem, M_mem, gen_pat, prng)
+        M_sum_test = M_mem.sum(axis=0)  # n_mut for each fold
+        U_sum_test = U_mem.sum(axis=0)
+        M_sum_train = sum(M_sum_test) - M_sum_test
+        U_sum_train = sum(U_sum_test) - U_sum_test
+        # per k-mer train counts: row total minus the fold (uint64, as the reference)
+        M_train = M_mem.sum(axis=1, keepdims=True) - M_mem
+        U_train = U_mem.sum(axis=1, keepdims=True) - U_mem
+        for a_i, alpha in enumerate(alphas):
+            betas = get_betas(alpha, M_sum_train, U_sum_train)
+            sum_train = _seq_sum_rows(test_folds(M_train, U_train, M_train, U_train, alpha, betas))
+            sum_test = _seq_sum_rows(test_folds(M_train, U_train, M_mem, U_mem, alpha, betas))
+            train_loss[a_i].extend(list(sum_train))
+            test_loss[a_i].extend(list(sum_test))
+    best_test_loss = 1e100
+    best_alpha = None
+    for a_i, alpha in enumerate(alphas):
+        test = sum(test_loss[a_i]) / nit
+        if args.verbosity > 0:
+            print(f'alpha={alpha} test_loss={test}', file=sys.stderr)
+        if test < best_test_loss:
+            best_alpha = alpha
+            best_test_loss = test
+    return best_alpha, best_test_loss

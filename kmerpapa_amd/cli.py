@@ -3,15 +3,16 @@
 
 The flow: read counts -> penalty presets -> general pattern (LCA) + zero fill ->
 (optional) grid cross-validation on the GPU -> final fit on the GPU -> partition table.
-Out of scope in this build: ``--greedy``, ``--greedyCV``, ``--BayesOpt``
-and ``--score all_kmers``; they are accepted by the parser and rejected with a message.
+Out of scope in this build (SURVEY.md §2): ``--greedy``, ``--greedyCV`` and ``--BayesOpt``;
+they are accepted by the parser and rejected with a message.  ``--score all_kmers`` (one
+rate per k-mer, no lattice DP) runs on the host (algorithms/all_kmers_CV.py).
 """
 import argparse
 import sys
 from math import log
 
 from . import __version__
-from .algorithms import bottum_up_array_penalty_plus_pseudo_CV, bottum_up_array_w_numba
+from .algorithms import all_kmers_CV, bottum_up_array_penalty_plus_pseudo_CV, bottum_up_array_w_numba
 from .io_utils import downsize_contextD, read_input
 from .papa import Pattern
 from .pattern_utils import LCA_pattern_of_kmers, get_M_U, matches
@@ -77,8 +78,6 @@ def get_parser():
 def _out_of_scope(args):
     if args.greedy or args.greedyCV or args.BayesOpt:
         return "--greedy / --greedyCV / --BayesOpt"
-    if args.score == "all_kmers":
-        return "--score all_kmers"
     return None
 
 
@@ -116,6 +115,8 @@ def main(args=None):
                    "LL": lambda: [0.0]}
         if args.score in presets:
             args.penalty_values = presets[args.score]()
+        elif args.score == "all_kmers":
+            pass
         elif args.score == "penalty_and_pseudo":
             args.penalty_values = [log(len(contextD))]  # before zero fill (cli.py:171-175)
             if verbose:
@@ -148,8 +149,14 @@ def main(args=None):
             if k != len(this_gen_pat):
                 this_contextD, this_gen_pat = downsize_contextD(this_contextD, this_gen_pat, k)
                 this_contextD = {key: tuple(v) for key, v in this_contextD.items()}
-            this_alpha, this_penalty, test_score = bottum_up_array_penalty_plus_pseudo_CV.pattern_partition_bottom_up(
-                this_gen_pat, this_contextD, args.pseudo_counts, args, n_mut, n_unmut, args.penalty_values)
+            if args.score == "all_kmers":
+                this_alpha, test_score = all_kmers_CV.all_kmers(this_gen_pat, this_contextD, args.pseudo_counts,
+                                                                args, n_mut, n_unmut)
+                this_penalty = None
+            else:
+                this_alpha, this_penalty, test_score = \
+                    bottum_up_array_penalty_plus_pseudo_CV.pattern_partition_bottom_up(
+                        this_gen_pat, this_contextD, args.pseudo_counts, args, n_mut, n_unmut, args.penalty_values)
             if test_score < best_score:
                 best_score, best_k, best_alpha, best_penalty = test_score, k, this_alpha, this_penalty
         if verbose:
@@ -163,7 +170,7 @@ def main(args=None):
     if best_alpha is None:
         assert len(args.pseudo_counts) == 1
         best_alpha = args.pseudo_counts[0]
-    if best_penalty is None:
+    if args.score != "all_kmers" and best_penalty is None:
         assert len(args.penalty_values) == 1
         best_penalty = args.penalty_values[0]
     if best_k is None:
@@ -177,8 +184,11 @@ def main(args=None):
     if verbose:
         print(f"Training on whole data set with k={best_k} alpha={best_alpha} penalty={best_penalty}",
               file=sys.stderr)
-    best_score, M, U, names = bottum_up_array_w_numba.pattern_partition_bottom_up(
-        gen_pat, contextD, best_alpha, best_beta, best_penalty, args, n_mut, n_unmut)
+    if args.score == "all_kmers":  # every k-mer is its own pattern (cli.py:266-271)
+        best_score, M, U, names = 0, n_mut, n_unmut, list(matches(gen_pat))
+    else:
+        best_score, M, U, names = bottum_up_array_w_numba.pattern_partition_bottom_up(
+            gen_pat, contextD, best_alpha, best_beta, best_penalty, args, n_mut, n_unmut)
 
     counts = [get_M_U(pat, contextD) for pat in names]
     # partition sanity checks of the reference (cli.py:289-292)

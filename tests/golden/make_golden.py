@@ -11,7 +11,7 @@ only numbers it produced.
 Canonical interpreter: /opt/conda/bin/python3.9 (numpy 1.26, scipy 1.7) which follows
 the numpy<2 promotion rules of the reference's pinned numpy 1.23.3.
 
-Usage:  python3 tests/golden/make_golden.py [--jobs small,grid5,fit5,cli5,fit7,cv7]
+Usage:  python3 tests/golden/make_golden.py [--jobs small,grid5,fit5,cli5,fit7,cv7,allk5]
 The GPU box never runs this file (no /root/reference there).
 """
 import argparse
@@ -337,6 +337,31 @@ def job_cli5(out):
             res[name] = {"argv": argv, "rc": rc, "output": open(o).read(),
                          "cvfile": open(f).read(), "stderr": err.getvalue()}
     with open(os.path.join(out, "cli5.json"), "w") as fh:
+        json.dump(res, fh)
+
+
+def job_allk5(out):
+    """--score all_kmers CLI runs on the 5-mer data (ref all_kmers_CV.py, cli.py:226-271)."""
+    import io as _io
+    import contextlib
+    from kmerpapa import cli
+    pos = os.path.join(REF_DATA, "mutated_5mers.txt")
+    bg = os.path.join(REF_DATA, "background_5mers.txt")
+    res = {}
+    with tempfile.TemporaryDirectory() as td:
+        runs = {
+            "grid": ["-p", pos, "-b", bg, "--score", "all_kmers", "-a", "0.5", "1", "10", "--nfolds", "5",
+                     "--seed", "1"],
+            "iter": ["-p", pos, "-b", bg, "--score", "all_kmers", "-a", "0.2", "3", "--nfolds", "3", "--seed", "7",
+                     "-i", "2", "-l"],
+        }
+        for name, argv in runs.items():
+            o = os.path.join(td, name + ".out")
+            err = _io.StringIO()
+            with contextlib.redirect_stderr(err):
+                rc = cli.main(argv + ["-o", o])
+            res[name] = {"argv": argv, "rc": rc, "output": open(o).read(), "stderr": err.getvalue()}
+    with open(os.path.join(out, "allk5.json"), "w") as fh:
         json.dump(res, fh)
 
 
