@@ -177,7 +177,8 @@ def main():
         cfg["gen_pat"] = a.pattern
     gen_pat = cfg["gen_pat"]
     prep = prepare(gen_pat, alphas=cfg["alphas"], penalties=cfg["penalties"], nfolds=cfg["nfolds"])
-    dev = engine.get_device(local)
+    ndev = engine.device_count()
+    dev = engine.get_device(local % max(1, ndev))  # one GPU per rank (several ranks per GPU only in rehearsals)
     t0 = time.time()
     plan = engine.Plan(dev, gen_pat, a.max_block)
     plan.set_counts(prep["Mk"], prep["Uk"])
@@ -234,7 +235,8 @@ def main():
         passes_full_cv = math.ceil(len(groups) / world)
         line = {
             "metric": "patterns scored/sec (lattice cells x folds x (alpha,c)), 9-mer 5-fold CV 5x5 grid"
-                      if a.config == "9mer" else f"patterns scored/sec, {a.config} config",
+                      if (a.config == "9mer" and not a.pattern) else
+                      f"patterns scored/sec, {a.config} config, general pattern {gen_pat}",
             "value": units / elapsed,
             "unit": "cell-scores/s",
             "n_gpus": world,
