@@ -81,7 +81,7 @@ struct kp_lowdesc {
     uint16_t l1, l2; // children of its first split (count recurrence); 0xFFFF for k-mer-low cells
     uint16_t kl;     // k-mer-low index (k-mer-low cells only)
     uint32_t info;   // packed low digits (4 bits per position)
-    uint32_t pad_;
+    uint32_t pl;     // low split pairs: (first 4-pair chunk in kp_plan's lpairs) << 8 | count
 };
 
 // ---------------------------------------------------------------------------
@@ -257,6 +257,18 @@ __host__ __device__ inline void kp_pairs_minv(SP st, uint32_t l, uint32_t cg, ui
         for (int j = 0; j < W; ++j) lmin[j] = fminf(lmin[j], va[p][j] + vb[p][j]);
 }
 
+// a cell's final score per lane: min(best split, single term)
+template <int W, typename SP>
+__host__ __device__ inline void kp_cell_store(SP row, const float *lmin, const kp_single_ctx &sc, const double *pen) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        float best = lmin[j];
+        const double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
+        if (s < (double)best) best = (float)s;  // float64 compare against the float32 store (CV :71)
+        row[j] = best;
+    }
+}
+
 // one DP cell for lanes j0 .. j0+W-1 of the NL lanes interleaved in LDS
 // (st[cell * NL + lane]); st[l] holds the best high-position split gathered from HBM.
 // pw = pair words [t][16]; pen = the W penalties of those lanes.  W = NL is the normal
@@ -301,13 +313,54 @@ __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint3
             }
         }
     }
+    kp_cell_store<W>(row, lmin, sc, pen);
+}
+
+// min over one 4-pair chunk of a cell's split-pair list (c1 | c2 << 16 per pair, kp_plan.h
+// lpairs) for W lanes from j0; all 8*W LDS reads issue before the first min
+template <int NL, int W, typename SP>
+__host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0, float *lmin) {
+    const uint32_t e[4] = {c.x, c.y, c.z, c.w};
+    float va[4][W], vb[4][W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) {
-        float best = lmin[j];
-        const double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
-        if (s < (double)best) best = (float)s;  // float64 compare against the float32 store (CV :71)
-        row[j] = best;
+    for (int p = 0; p < 4; ++p) {
+        const uint32_t c1 = e[p] & 0xFFFFu, c2 = e[p] >> 16;
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            va[p][j] = st[c1 * NL + j0 + j];
+            vb[p][j] = st[c2 * NL + j0 + j];
+        }
     }
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int j = 0; j < W; ++j) lmin[j] = fminf(lmin[j], va[p][j] + vb[p][j]);
+}
+
+#define KP_PRE_CHUNKS 4  // pair-list chunks a thread loads ahead (16 pairs; longer lists load the rest on use)
+
+// The same cell from its flat split-pair list (the sweep kernel's form): npairs pairs in
+// 4-pair chunks, the first KP_PRE_CHUNKS already loaded into pre[] by the caller (so the
+// loads overlap the logs), the rest read from lp.  The wave runs as many chunks as its
+// longest list; shorter lists end in (B, B) pairs that read the +inf slot B.
+template <int NL, int W, typename SP>
+__host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, const uint4 *pre, const uint4 *lp, SP st,
+                                                const kp_single_ctx &sc, double alpha, double beta,
+                                                const double *pen, uint32_t j0 = 0) {
+    SP row = st + l * NL + j0;
+    if (sc.kmer) {  // level 0 (CV :145-151 / Fit :106-114)
+#pragma unroll
+        for (int j = 0; j < W; ++j) row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
+        return;
+    }
+    float lmin[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) lmin[j] = row[j];
+#pragma unroll
+    for (int k = 0; k < KP_PRE_CHUNKS; ++k)
+        if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
+    for (uint32_t k = KP_PRE_CHUNKS; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+    kp_cell_store<W>(row, lmin, sc, pen);
 }
 
 // ---------------------------------------------------------------------------

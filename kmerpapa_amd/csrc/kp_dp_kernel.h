@@ -26,6 +26,7 @@ struct kp_dev_tables {
     const uint64_t *pw;
     const uint64_t *hdig;
     const uint8_t *lowmask;
+    const uint4 *lpairs;  // low split-pair lists in 4-pair chunks (kp_plan.h lpairs)
 };
 
 struct kp_dp_params {
@@ -172,6 +173,13 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
             const float4 b0 = *reinterpret_cast<const float4 *>(base + hp[p].h2);
             kp_min4v(best, a0, b0);
         }
+        if (4 * c + 4 > g.B) {  // the chunk with the pad slots: slot B is the +inf cell of
+            const float inf = __builtin_huge_valf();  // padded pair lists (kp_dp_cell_list)
+            if (4 * c + 0 >= g.B) best.x = inf;
+            if (4 * c + 1 >= g.B) best.y = inf;
+            if (4 * c + 2 >= g.B) best.z = inf;
+            if (4 * c + 3 >= g.B) best.w = inf;
+        }
         float *sl = st + (size_t)(4 * c) * NL + ll;
         sl[0] = best.x;
         sl[NL] = best.y;
@@ -224,6 +232,12 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
             if (q < cnt && !(P.dbg & 8)) {
                 const uint32_t l = cur[0].x & 0xFFFFu;
                 const uint32_t info = cur[0].z;
+                const uint32_t npairs = cur[0].w & 0xFFu;
+                const uint4 *lp = P.T.lpairs + (cur[0].w >> 8);
+                uint4 pre[KP_PRE_CHUNKS];
+#pragma unroll
+                for (int c = 0; c < KP_PRE_CHUNKS; ++c)
+                    if (4u * c < npairs) pre[c] = lp[c];
                 kp_single_ctx sc;
                 kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
                 sc.kmer = high_zero && lam == 0;
@@ -235,8 +249,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                     sc.log1mp = log(1.0 - pr);
                 }
                 const double pj = G->pen[j];
-                kp_dp_cell_values<NL, 1>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta, &pj,
-                                         j);
+                kp_dp_cell_list<NL, 1>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, &pj, j);
             }
         } else
 #pragma unroll
@@ -245,6 +258,14 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
             if (q < cnt) {
                 const uint32_t l = cur[k].x & 0xFFFFu;
                 const uint32_t info = cur[k].z;
+                // the cell's split-pair list (plan tables, L2-resident): issued before the
+                // logs so the loads overlap them
+                const uint32_t npairs = cur[k].w & 0xFFu;
+                const uint4 *lp = P.T.lpairs + (cur[k].w >> 8);
+                uint4 pre[KP_PRE_CHUNKS];
+#pragma unroll
+                for (int c = 0; c < KP_PRE_CHUNKS; ++c)
+                    if (4u * c < npairs) pre[c] = lp[c];
                 // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
                 kp_single_ctx sc;
                 kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
@@ -257,8 +278,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                     sc.log1mp = log(1.0 - pr);
                 }
                 if (!(P.dbg & 8)) {
-                    kp_dp_cell_values<NL, NL>(g, (const kp_lds_u64 *)pw, l, info, (kp_lds_f32 *)st, sc, alpha, beta,
-                                              pen);
+                    kp_dp_cell_list<NL, NL>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, pen);
                 } else {  // timing ablation: no split scan, keep the single term
 #pragma unroll
                     for (int j = 0; j < NL; ++j)

@@ -373,6 +373,7 @@ struct kp_plan {
     uint64_t *d_pw = nullptr;
     uint64_t *d_hdig = nullptr;
     uint8_t *d_lowmask = nullptr;
+    uint32_t *d_lpairs = nullptr;
     // counts
     void *d_K = nullptr;
     int nf = 0;
@@ -409,6 +410,7 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     T.pw = p->d_pw;
     T.hdig = p->d_hdig;
     T.lowmask = p->d_lowmask;
+    T.lpairs = reinterpret_cast<const uint4 *>(p->d_lpairs);
     return T;
 }
 
@@ -488,7 +490,8 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
         (rc = upload(&p->d_loff, p->hp.loff)) || (rc = upload(&p->d_klofs, p->hp.klofs)) ||
         (rc = upload(&p->d_kllist, p->hp.kllist)) || (rc = upload(&p->d_hlist, p->hp.hlist)) ||
         (rc = upload(&p->d_ldesc, p->hp.ldesc)) || (rc = upload(&p->d_pw, p->hp.pw)) ||
-        (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_lowmask, p->hp.lowmask))) {
+        (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_lowmask, p->hp.lowmask)) ||
+        (rc = upload(&p->d_lpairs, p->hp.lpairs))) {
         kp_plan_destroy(p);
         return rc;
     }
@@ -500,7 +503,7 @@ void kp_plan_destroy(kp_plan *p) {
     if (!p) return;
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
     void *bufs[] = {p->d_tabs,    p->d_lowinfo, p->d_loff,   p->d_klofs,   p->d_kllist, p->d_hlist, p->d_ldesc,
-                    p->d_pw,      p->d_hdig,    p->d_lowmask, p->d_K,      p->d_S,      p->d_nodes, p->d_groups,
+                    p->d_pw,      p->d_hdig,    p->d_lowmask, p->d_lpairs, p->d_K,      p->d_S,      p->d_nodes, p->d_groups,
                     p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
                     p->d_leaves};
     for (void *b : bufs) dfree(b);

@@ -47,6 +47,8 @@ struct host_plan {
     std::vector<uint16_t> lorder;      // [B] low cells sorted by low level
     std::vector<int32_t> loff;         // [lmax + 2]
     std::vector<kp_lowdesc> ldesc;     // [B] low cells in level order
+    std::vector<uint32_t> lpairs;      // low split pairs of every cell, in 4-pair chunks (kp_lowdesc.pl)
+    uint32_t max_low_pairs = 0;        // most low split pairs of one cell
     std::vector<uint16_t> kl2l;        // [n_kl] k-mer-low index -> low cell
     std::vector<uint32_t> klofs;       // [B + 1]
     std::vector<uint16_t> kllist;      // k-mer-low cells matching each low cell
@@ -105,7 +107,7 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     g.t = t;
     g.kh = k - t;
     g.B = (uint32_t)(t < k ? g.cgl[t] : acc);
-    g.Bpad = (g.B + 15u) & ~15u;
+    g.Bpad = (g.B + 16u) & ~15u;  // >= B + 1: slot B is the +inf cell of padded pair lists
     g.nblocks = acc / g.B;
     uint32_t nkl = 1;
     for (int i = 0; i < t; ++i) nkl *= g.n[i];
@@ -166,17 +168,29 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     P.lorder.resize(B);
     {
         // inside a level any order is valid (cells only read lower levels); cells are
-        // grouped by their split signature (pairs at each low position) so that the 64
-        // cells of a wave run the same pair loops (no divergence in the level phase)
-        std::vector<uint64_t> key(B);
+        // sorted by their number of low split pairs, then by split signature, so that the
+        // 64 cells of a wave run (nearly) the same number of pair chunks in the level phase
+        std::vector<uint32_t> npairs(B);
+        std::vector<uint64_t> sigs(B);
         for (uint32_t l = 0; l < B; ++l) {
             uint64_t sig = 0;
-            for (int i = 0; i < t; ++i) sig = sig * 8 + P.tabs[i].np[kp_low_digit(P.lowinfo[l], i)];
-            key[l] = ((uint64_t)llev[l] << 48) | (sig << 16) | l;
+            uint32_t np = 0;
+            for (int i = 0; i < t; ++i) {
+                const uint32_t n = P.tabs[i].np[kp_low_digit(P.lowinfo[l], i)];
+                sig = sig * 8 + n;
+                np += n;
+            }
+            sigs[l] = sig;
+            npairs[l] = np;
         }
         std::vector<uint32_t> idx(B);
         for (uint32_t l = 0; l < B; ++l) idx[l] = l;
-        std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+        std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+            if (llev[a] != llev[b]) return llev[a] < llev[b];
+            if (npairs[a] != npairs[b]) return npairs[a] < npairs[b];
+            if (sigs[a] != sigs[b]) return sigs[a] < sigs[b];
+            return a < b;
+        });
         for (uint32_t q = 0; q < B; ++q) P.lorder[q] = (uint16_t)idx[q];
     }
     // level-ordered descriptors: first split pair (count recurrence) and k-mer-low index
@@ -207,6 +221,24 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
                 }
             }
         }
+        // the cell's low split pairs as child-cell pairs (c1 | c2 << 16), position by
+        // position in scan order, padded to whole 4-pair chunks with (B, B): slot B of the
+        // block holds +inf in every lane, so padding never wins a min
+        const uint32_t first = (uint32_t)P.lpairs.size();
+        uint32_t np = 0;
+        for (int i = 0; i < t; ++i) {
+            const uint32_t d = kp_low_digit(D.info, i);
+            for (uint32_t p = 0; p < P.tabs[i].np[d]; ++p) {
+                const uint32_t c1 = l - (d - P.tabs[i].pa[d][p]) * (uint32_t)g.cgl[i];
+                const uint32_t c2 = l - (d - P.tabs[i].pb[d][p]) * (uint32_t)g.cgl[i];
+                P.lpairs.push_back(c1 | (c2 << 16));
+                ++np;
+            }
+        }
+        while (P.lpairs.size() & 3u) P.lpairs.push_back(B | (B << 16));
+        if (np > 255 || (first >> 2) > 0xFFFFFFu) return "too many low split pairs";
+        D.pl = ((first >> 2) << 8) | np;
+        P.max_low_pairs = std::max(P.max_low_pairs, np);
         P.ldesc[q] = D;
     }
     // nucleotide index sets of every (position, digit): nucleotide c of code x has

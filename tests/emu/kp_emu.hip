@@ -18,17 +18,17 @@
 namespace {
 std::string g_err;
 
-void cell_values(int nl, const kp_geom &g, const uint64_t *pw, uint32_t l, uint32_t info, float *st,
-                 const kp_single_ctx &sc, double a, double b, const double *pen) {
+void cell_values(int nl, uint32_t l, uint32_t npairs, const uint4 *lp, float *st, const kp_single_ctx &sc, double a,
+                 double b, const double *pen) {
     switch (nl) {
-        case 1: kp_dp_cell_values<1, 1>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 2: kp_dp_cell_values<2, 2>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 3: kp_dp_cell_values<3, 3>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 4: kp_dp_cell_values<4, 4>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 5: kp_dp_cell_values<5, 5>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 6: kp_dp_cell_values<6, 6>(g, pw, l, info, st, sc, a, b, pen); break;
-        case 7: kp_dp_cell_values<7, 7>(g, pw, l, info, st, sc, a, b, pen); break;
-        default: kp_dp_cell_values<8, 8>(g, pw, l, info, st, sc, a, b, pen); break;
+        case 1: kp_dp_cell_list<1, 1>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 2: kp_dp_cell_list<2, 2>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 3: kp_dp_cell_list<3, 3>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 4: kp_dp_cell_list<4, 4>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 5: kp_dp_cell_list<5, 5>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 6: kp_dp_cell_list<6, 6>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 7: kp_dp_cell_list<7, 7>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        default: kp_dp_cell_list<8, 8>(l, npairs, lp, lp, st, sc, a, b, pen); break;
     }
 }
 
@@ -96,7 +96,7 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
                         for (int p = 0; p < np; ++p)
                             best = fminf(best, S[kp_lane_row(g, hpairs[p].h1, lane) + l] +
                                                    S[kp_lane_row(g, hpairs[p].h2, lane) + l]);
-                        st[(size_t)l * G.nl + ll] = best;
+                        st[(size_t)l * G.nl + ll] = l < g.B ? best : __builtin_huge_valf();  // pad slot: +inf
                     }
                 }
                 // levels (same descriptor table, count table and cell function as kp_dp_kernel)
@@ -113,7 +113,8 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
                             sc.logp = log(p);
                             sc.log1mp = log(1.0 - p);
                         }
-                        cell_values(G.nl, g, hp.pw.data(), D.l, D.info, st.data(), sc, G.alpha, G.beta, G.pen);
+                        const uint4 *lp = reinterpret_cast<const uint4 *>(hp.lpairs.data()) + (D.pl >> 8);
+                        cell_values(G.nl, D.l, D.pl & 0xFFu, lp, st.data(), sc, G.alpha, G.beta, G.pen);
                     }
                 }
                 // store
