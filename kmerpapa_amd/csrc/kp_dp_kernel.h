@@ -65,6 +65,13 @@ struct kp_dp_params {
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
 
+// a workgroup-uniform 64-bit value (read by every lane from the same LDS word) into SGPRs
+__device__ inline uint64_t kp_rfl64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // float4 min-update with a split candidate a + b (fminf drops NaN candidates like "<")
 __device__ inline void kp_min4v(float4 &best, const float4 a, const float4 b) {
     best.x = fminf(best.x, a.x + b.x);
@@ -146,45 +153,65 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     KP_STAMP(0);
 
     // ---- gather: high-position splits, as whole child-block rows (value only) ----
-    const uint32_t nch = Bpad / 4;
-    for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
-        const uint32_t ll = item / nch, c = item % nch;
-        const uint64_t lrow = (uint64_t)(lane0 + ll) * Bpad + 4 * c;
-        const float *base = P.S + lrow;
-        float4 best = make_float4(__builtin_huge_valf(), __builtin_huge_valf(), __builtin_huge_valf(),
-                                  __builtin_huge_valf());
+    // Each thread takes two float4 items (4 cells of one lane) at a time, so up to 16
+    // row loads are in flight per thread even when the block has few pairs.  A pair's
+    // child-row offsets are workgroup-uniform: read into SGPRs, so each load is a scalar
+    // base plus a 32-bit lane offset.
+    const uint32_t nch = Bpad / 4, nitems = (uint32_t)NL * nch;
+    auto pad_inf = [&](float4 &b, uint32_t c) {  // slot B: the +inf cell of padded pair lists
+        if (4 * c + 4 > g.B) {
+            const float inf = __builtin_huge_valf();
+            if (4 * c + 0 >= g.B) b.x = inf;
+            if (4 * c + 1 >= g.B) b.y = inf;
+            if (4 * c + 2 >= g.B) b.z = inf;
+            if (4 * c + 3 >= g.B) b.w = inf;
+        }
+    };
+    for (uint32_t it0 = threadIdx.x; it0 < nitems; it0 += 2 * blockDim.x) {
+        const uint32_t it1 = (it0 + blockDim.x < nitems) ? it0 + blockDim.x : it0;
+        const uint32_t ll0 = it0 / nch, c0 = it0 % nch, ll1 = it1 / nch, c1 = it1 % nch;
+        const uint32_t o0 = (lane0 + ll0) * Bpad + 4 * c0, o1 = (lane0 + ll1) * Bpad + 4 * c1;
+        const float inf = __builtin_huge_valf();
+        float4 best0 = make_float4(inf, inf, inf, inf), best1 = best0;
         int p = 0;
         for (; p + 4 <= np; p += 4) {
-            const float4 a0 = *reinterpret_cast<const float4 *>(base + hp[p].h1);
-            const float4 b0 = *reinterpret_cast<const float4 *>(base + hp[p].h2);
-            const float4 a1 = *reinterpret_cast<const float4 *>(base + hp[p + 1].h1);
-            const float4 b1 = *reinterpret_cast<const float4 *>(base + hp[p + 1].h2);
-            const float4 a2 = *reinterpret_cast<const float4 *>(base + hp[p + 2].h1);
-            const float4 b2 = *reinterpret_cast<const float4 *>(base + hp[p + 2].h2);
-            const float4 a3 = *reinterpret_cast<const float4 *>(base + hp[p + 3].h1);
-            const float4 b3 = *reinterpret_cast<const float4 *>(base + hp[p + 3].h2);
-            kp_min4v(best, a0, b0);
-            kp_min4v(best, a1, b1);
-            kp_min4v(best, a2, b2);
-            kp_min4v(best, a3, b3);
+            const float *r[8];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                r[2 * q] = P.S + kp_rfl64(hp[p + q].h1);
+                r[2 * q + 1] = P.S + kp_rfl64(hp[p + q].h2);
+            }
+            float4 v0[8], v1[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                v0[q] = *reinterpret_cast<const float4 *>(r[q] + o0);
+                v1[q] = *reinterpret_cast<const float4 *>(r[q] + o1);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                kp_min4v(best0, v0[2 * q], v0[2 * q + 1]);
+                kp_min4v(best1, v1[2 * q], v1[2 * q + 1]);
+            }
         }
         for (; p < np; ++p) {
-            const float4 a0 = *reinterpret_cast<const float4 *>(base + hp[p].h1);
-            const float4 b0 = *reinterpret_cast<const float4 *>(base + hp[p].h2);
-            kp_min4v(best, a0, b0);
+            const float *ra = P.S + kp_rfl64(hp[p].h1), *rb = P.S + kp_rfl64(hp[p].h2);
+            kp_min4v(best0, *reinterpret_cast<const float4 *>(ra + o0), *reinterpret_cast<const float4 *>(rb + o0));
+            kp_min4v(best1, *reinterpret_cast<const float4 *>(ra + o1), *reinterpret_cast<const float4 *>(rb + o1));
         }
-        if (4 * c + 4 > g.B) {  // the chunk with the pad slots: slot B is the +inf cell of
-            const float inf = __builtin_huge_valf();  // padded pair lists (kp_dp_cell_list)
-            if (4 * c + 0 >= g.B) best.x = inf;
-            if (4 * c + 1 >= g.B) best.y = inf;
-            if (4 * c + 2 >= g.B) best.z = inf;
-            if (4 * c + 3 >= g.B) best.w = inf;
+        pad_inf(best0, c0);
+        pad_inf(best1, c1);
+        float *sl = st + (size_t)(4 * c0) * NL + ll0;
+        sl[0] = best0.x;
+        sl[NL] = best0.y;
+        sl[2 * NL] = best0.z;
+        sl[3 * NL] = best0.w;
+        if (it1 != it0) {
+            sl = st + (size_t)(4 * c1) * NL + ll1;
+            sl[0] = best1.x;
+            sl[NL] = best1.y;
+            sl[2 * NL] = best1.z;
+            sl[3 * NL] = best1.w;
         }
-        float *sl = st + (size_t)(4 * c) * NL + ll;
-        sl[0] = best.x;
-        sl[NL] = best.y;
-        sl[2 * NL] = best.z;
-        sl[3 * NL] = best.w;
     }
     __syncthreads();
     KP_STAMP(1);
