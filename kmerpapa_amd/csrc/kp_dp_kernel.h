@@ -80,6 +80,70 @@ __device__ inline void kp_min4v(float4 &best, const float4 a, const float4 b) {
     best.w = fminf(best.w, a.w + b.w);
 }
 
+// Gather phase of one block: st[cell][lane] = min over the block's high split pairs of
+// S[child1] + S[child2], for the NL lanes.  Items are float4 runs (4 cells of one lane);
+// each thread takes NI items at a time (NI * 2 * min(np, PU) row loads in flight).  A
+// pair's child-row offsets are workgroup-uniform: read into SGPRs, so each load is a
+// scalar base plus a 32-bit lane offset.  Slot B (padding) becomes +inf: the cell that
+// padded pair lists point at (kp_dp_cell_list).
+template <int NL, int NI, int PU = 4>
+__device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp, int np, uint32_t lane0, float *st) {
+    const kp_geom &g = P.g;
+    const uint32_t Bpad = g.Bpad, nch = Bpad / 4, nitems = (uint32_t)NL * nch;
+    const float inf = __builtin_huge_valf();
+    for (uint32_t it0 = threadIdx.x; it0 < nitems; it0 += NI * blockDim.x) {
+        uint32_t it[NI], o[NI];
+        float4 best[NI];
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            it[i] = (it0 + i * blockDim.x < nitems) ? it0 + i * blockDim.x : it0;
+            o[i] = (lane0 + it[i] / nch) * Bpad + 4 * (it[i] % nch);
+            best[i] = make_float4(inf, inf, inf, inf);
+        }
+        int p = 0;
+        for (; p + PU <= np; p += PU) {
+            const float *r[2 * PU];
+#pragma unroll
+            for (int q = 0; q < PU; ++q) {
+                r[2 * q] = P.S + kp_rfl64(hp[p + q].h1);
+                r[2 * q + 1] = P.S + kp_rfl64(hp[p + q].h2);
+            }
+            float4 v[NI][2 * PU];
+#pragma unroll
+            for (int q = 0; q < 2 * PU; ++q)
+#pragma unroll
+                for (int i = 0; i < NI; ++i) v[i][q] = *reinterpret_cast<const float4 *>(r[q] + o[i]);
+#pragma unroll
+            for (int q = 0; q < PU; ++q)
+#pragma unroll
+                for (int i = 0; i < NI; ++i) kp_min4v(best[i], v[i][2 * q], v[i][2 * q + 1]);
+        }
+        for (; p < np; ++p) {
+            const float *ra = P.S + kp_rfl64(hp[p].h1), *rb = P.S + kp_rfl64(hp[p].h2);
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+                kp_min4v(best[i], *reinterpret_cast<const float4 *>(ra + o[i]),
+                         *reinterpret_cast<const float4 *>(rb + o[i]));
+        }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            if (i > 0 && it[i] == it0) break;
+            const uint32_t ll = it[i] / nch, c = it[i] % nch;
+            if (4 * c + 4 > g.B) {
+                if (4 * c + 0 >= g.B) best[i].x = inf;
+                if (4 * c + 1 >= g.B) best[i].y = inf;
+                if (4 * c + 2 >= g.B) best[i].z = inf;
+                if (4 * c + 3 >= g.B) best[i].w = inf;
+            }
+            float *sl = st + (size_t)(4 * c) * NL + ll;
+            sl[0] = best[i].x;
+            sl[NL] = best[i].y;
+            sl[2 * NL] = best[i].z;
+            sl[3 * NL] = best[i].w;
+        }
+    }
+}
+
 template <typename CT, int NL>
 __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -153,66 +217,9 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     KP_STAMP(0);
 
     // ---- gather: high-position splits, as whole child-block rows (value only) ----
-    // Each thread takes two float4 items (4 cells of one lane) at a time, so up to 16
-    // row loads are in flight per thread even when the block has few pairs.  A pair's
-    // child-row offsets are workgroup-uniform: read into SGPRs, so each load is a scalar
-    // base plus a 32-bit lane offset.
-    const uint32_t nch = Bpad / 4, nitems = (uint32_t)NL * nch;
-    auto pad_inf = [&](float4 &b, uint32_t c) {  // slot B: the +inf cell of padded pair lists
-        if (4 * c + 4 > g.B) {
-            const float inf = __builtin_huge_valf();
-            if (4 * c + 0 >= g.B) b.x = inf;
-            if (4 * c + 1 >= g.B) b.y = inf;
-            if (4 * c + 2 >= g.B) b.z = inf;
-            if (4 * c + 3 >= g.B) b.w = inf;
-        }
-    };
-    for (uint32_t it0 = threadIdx.x; it0 < nitems; it0 += 2 * blockDim.x) {
-        const uint32_t it1 = (it0 + blockDim.x < nitems) ? it0 + blockDim.x : it0;
-        const uint32_t ll0 = it0 / nch, c0 = it0 % nch, ll1 = it1 / nch, c1 = it1 % nch;
-        const uint32_t o0 = (lane0 + ll0) * Bpad + 4 * c0, o1 = (lane0 + ll1) * Bpad + 4 * c1;
-        const float inf = __builtin_huge_valf();
-        float4 best0 = make_float4(inf, inf, inf, inf), best1 = best0;
-        int p = 0;
-        for (; p + 4 <= np; p += 4) {
-            const float *r[8];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                r[2 * q] = P.S + kp_rfl64(hp[p + q].h1);
-                r[2 * q + 1] = P.S + kp_rfl64(hp[p + q].h2);
-            }
-            float4 v0[8], v1[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                v0[q] = *reinterpret_cast<const float4 *>(r[q] + o0);
-                v1[q] = *reinterpret_cast<const float4 *>(r[q] + o1);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                kp_min4v(best0, v0[2 * q], v0[2 * q + 1]);
-                kp_min4v(best1, v1[2 * q], v1[2 * q + 1]);
-            }
-        }
-        for (; p < np; ++p) {
-            const float *ra = P.S + kp_rfl64(hp[p].h1), *rb = P.S + kp_rfl64(hp[p].h2);
-            kp_min4v(best0, *reinterpret_cast<const float4 *>(ra + o0), *reinterpret_cast<const float4 *>(rb + o0));
-            kp_min4v(best1, *reinterpret_cast<const float4 *>(ra + o1), *reinterpret_cast<const float4 *>(rb + o1));
-        }
-        pad_inf(best0, c0);
-        pad_inf(best1, c1);
-        float *sl = st + (size_t)(4 * c0) * NL + ll0;
-        sl[0] = best0.x;
-        sl[NL] = best0.y;
-        sl[2 * NL] = best0.z;
-        sl[3 * NL] = best0.w;
-        if (it1 != it0) {
-            sl = st + (size_t)(4 * c1) * NL + ll1;
-            sl[0] = best1.x;
-            sl[NL] = best1.y;
-            sl[2 * NL] = best1.z;
-            sl[3 * NL] = best1.w;
-        }
-    }
+    // four float4 items per thread at a time, two pairs per step: 16 row loads in flight
+    // per thread even when the block has few pairs (measured best of 1-4 items x 1-4 pairs)
+    kp_gather_items<NL, 4, 2>(P, hp, np, lane0, st);
     __syncthreads();
     KP_STAMP(1);
 
@@ -320,6 +327,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     }
 
     // ---- store the block's score rows ----
+    const uint32_t nch = Bpad / 4;
     for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
         const uint32_t ll = item / nch, c = item % nch;
         const float *sl = st + (size_t)(4 * c) * NL + ll;
