@@ -23,6 +23,8 @@
  *   kp_fit_leaves    backtrack(gen_pat, ...) Fit :17-24, 121
  *   kp_fold_split    CV_tools.py sample :5-27 and the fold loop of
  *                    make_all_folds_contextD_patterns :44-57 (host code, numpy legacy RNG)
+ *   kp_kmer_parse    io_utils.py read_dict :82-136 (with downsize_contextD's centring,
+ *                    :50-79) and read_joint_kmer_counts :3-46 (host code)
  */
 #ifndef KMERPAPA_HIP_H
 #define KMERPAPA_HIP_H
@@ -119,6 +121,27 @@ int kp_dump_lane(kp_plan *plan, uint32_t lane, float *score, uint8_t *code);
  * colors[n] = ball counts per colour; folds[n][nf] receives each colour's fold counts
  * (folds 0..nf-2 sampled, the last takes the remainder). */
 int kp_fold_split(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uint64_t n, int nf, uint64_t *folds);
+
+/* k-mer count text (host code, no GPU).  Parses `nbytes` of file text into a table of
+ * unique k-mers as 2-bit codes (A=0 C=1 G=2 T=3, first letter most significant: code
+ * order = sorted k-mer order) with counts:
+ *   columns = 2: "kmer count" lines (io_utils.read_dict :82-136).  Counts of equal k-mers
+ *     are summed into c0 (c1 = 0); total0 = sum of kept counts.  length > 0 keeps the
+ *     central `length` letters (width//2 - length//2 ...); with a super pattern and
+ *     length <= 0 the pattern's length is used.  Negative counts are an error.
+ *   columns = 3: "kmer positive background" lines (read_joint_kmer_counts :3-46).  The
+ *     last line of a k-mer wins: c0 = positive, c1 = background - positive (an error if
+ *     negative); total0 = n_negative_total, total1 = n_positive_total over every kept line.
+ * super_pattern (IUPAC, may be NULL or "") keeps only matching k-mers.  Lines whose k-mer
+ * has a letter other than A/C/G/T are skipped; a line with the wrong number of tokens,
+ * a bad count or k-mers of different lengths is KP_E_ARG with kp_last_error() text. */
+typedef struct kp_kmer_table kp_kmer_table;
+int kp_kmer_parse(const char *text, uint64_t nbytes, int columns, const char *super_pattern, int length,
+                  kp_kmer_table **out);
+int kp_kmer_table_info(const kp_kmer_table *t, uint64_t *n, int32_t *k, int64_t *total0, int64_t *total1);
+/* codes[n], c0[n], c1[n]: caller-allocated (n from kp_kmer_table_info) */
+int kp_kmer_table_copy(const kp_kmer_table *t, uint64_t *codes, int64_t *c0, int64_t *c1);
+void kp_kmer_table_free(kp_kmer_table *t);
 
 #ifdef __cplusplus
 }

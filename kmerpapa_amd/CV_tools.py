@@ -11,7 +11,7 @@ C-ABI uploads (``kp_set_counts``).
 """
 import numpy as np
 
-from .pattern_utils import PatternEnumeration, matches
+from .pattern_utils import PatternEnumeration, generality, matches
 
 
 def sample(m, colors, itype, prng):
@@ -70,13 +70,18 @@ def fold_tables(contextD, n_folds, prng, itype=np.uint64):
     Returns ``(contexts, M, U)`` with ``M, U`` of shape ``[n_kmers, n_folds]``: exactly the
     level-0 rows :func:`make_all_folds_contextD_patterns` scatters into ``M_mem``/``U_mem``.
     """
-    contexts = sorted(contextD)
-    nk = len(contexts)
-    colors = np.empty(2 * nk, dtype=itype)
-    for i, c in enumerate(contexts):
-        nm, nu = contextD[c]
-        colors[i] = nm
-        colors[nk + i] = nu
+    if hasattr(contextD, "letters"):  # io_utils.KmerCounts: already in sorted order, as arrays
+        contexts = contextD
+        colors = np.concatenate([contextD.M, contextD.U]).astype(itype)
+        nk = len(contexts)
+    else:
+        contexts = sorted(contextD)
+        nk = len(contexts)
+        colors = np.empty(2 * nk, dtype=itype)
+        for i, c in enumerate(contexts):
+            nm, nu = contextD[c]
+            colors[i] = nm
+            colors[nk + i] = nu
     folds = _split_colors(colors, n_folds, itype, prng)
     return contexts, folds[:nk], folds[nk:]
 
@@ -93,13 +98,23 @@ def make_all_folds_contextD_patterns(contextD, U_mem, M_mem, general_pattern, pr
 
 def make_all_folds_contextD_kmers(contextD, U_mem, M_mem, general_pattern, prng):
     """Fold counts for every k-mer of ``general_pattern`` in :func:`matches` order (ref :65-96)."""
-    contexts = list(matches(general_pattern))
-    nk = len(contexts)
-    colors = np.zeros(2 * nk, dtype=np.uint64)
-    for i, c in enumerate(contexts):
-        nm, nu = contextD[c]
-        colors[i] = nm
-        colors[nk + i] = nu
+    if hasattr(contextD, "letters"):  # io_utils.KmerCounts: matches() order = KmerEnumeration order
+        from .engine import kmer_order
+        nk = generality(general_pattern)
+        idx = kmer_order(general_pattern, contextD)
+        if len(contextD) != nk:
+            raise KeyError("the count table must hold every k-mer of the general pattern (zero-filled)")
+        colors = np.zeros(2 * nk, dtype=np.uint64)
+        colors[idx] = contextD.M
+        colors[nk + idx] = contextD.U
+    else:
+        contexts = list(matches(general_pattern))
+        nk = len(contexts)
+        colors = np.zeros(2 * nk, dtype=np.uint64)
+        for i, c in enumerate(contexts):
+            nm, nu = contextD[c]
+            colors[i] = nm
+            colors[nk + i] = nu
     folds = _split_colors(colors, U_mem.shape[1], np.uint64, prng)
     M_mem[:nk] = folds[:nk]
     U_mem[:nk] = folds[nk:]

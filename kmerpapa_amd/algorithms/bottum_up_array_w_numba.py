@@ -21,9 +21,12 @@ def _itype(nmut, nunmut):
 
 def fit_partition(gen_pat, contextD, alpha, beta, penalty, itype, index_mut=0, device=None, max_block=0):
     """Run the Fit DP; returns ``(score f32, M_root, U_root, leaf cell indices)``."""
-    contexts = list(contextD.keys())
-    M = np.array([contextD[c][index_mut] for c in contexts], dtype=itype)
-    U = np.array([contextD[c][-1] for c in contexts], dtype=itype)
+    if hasattr(contextD, "letters") and index_mut == 0:  # io_utils.KmerCounts (native reader)
+        contexts, M, U = contextD, contextD.M.astype(itype), contextD.U.astype(itype)
+    else:
+        contexts = list(contextD.keys())
+        M = np.array([contextD[c][index_mut] for c in contexts], dtype=itype)
+        U = np.array([contextD[c][-1] for c in contexts], dtype=itype)
     Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, M, U, generality(gen_pat), itype)
     dev = engine.visible_devices()[0] if device is None else device
     plan = engine.get_plan(dev, gen_pat, max_block)

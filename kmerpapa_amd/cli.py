@@ -13,9 +13,9 @@ from math import log
 
 from . import __version__
 from .algorithms import all_kmers_CV, bottum_up_array_penalty_plus_pseudo_CV, bottum_up_array_w_numba
-from .io_utils import downsize_contextD, read_input
+from .io_utils import read_input_table
 from .papa import Pattern
-from .pattern_utils import LCA_pattern_of_kmers, get_M_U, matches
+from .pattern_utils import matches
 from .score_utils import get_loss
 
 
@@ -95,7 +95,7 @@ def main(args=None):
         return 2
     super_pattern = Pattern(args.super_pattern) if args.super_pattern is not None else None
     try:
-        contextD, n_unmut, n_mut = read_input(args, super_pattern)
+        contextD, n_unmut, n_mut = read_input_table(args, super_pattern)  # native reader (io_utils)
     except Exception as e:  # the reference prints help and returns 0 on bad input (cli.py:144-153)
         parser.print_help()
         print("=" * 80, file=sys.stderr)
@@ -124,12 +124,10 @@ def main(args=None):
         else:
             raise AssertionError(f"illegal score option {args.score}")
 
-    gen_pat = LCA_pattern_of_kmers(list(contextD.keys()))
+    gen_pat = contextD.lca_pattern()  # LCA_pattern_of_kmers over the table (cli.py:180)
     if args.super_pattern is not None:
         assert gen_pat == args.super_pattern
-    for context in matches(gen_pat):
-        if context not in contextD:
-            contextD[context] = (0, 0)
+    contextD = contextD.zero_filled(gen_pat)  # every k-mer of gen_pat, missing ones (0, 0) (cli.py:185-187)
     if verbose:
         print(f"General pattern: {gen_pat}", file=sys.stderr)
     if args.CVfile is not None:
@@ -147,8 +145,7 @@ def main(args=None):
             if verbose:
                 print(f"Running {args.nfolds}-fold cross validation on {k}-mers", file=sys.stderr)
             if k != len(this_gen_pat):
-                this_contextD, this_gen_pat = downsize_contextD(this_contextD, this_gen_pat, k)
-                this_contextD = {key: tuple(v) for key, v in this_contextD.items()}
+                this_contextD, this_gen_pat = this_contextD.downsized(this_gen_pat, k)  # downsize_contextD
             if args.score == "all_kmers":
                 this_alpha, test_score = all_kmers_CV.all_kmers(this_gen_pat, this_contextD, args.pseudo_counts,
                                                                 args, n_mut, n_unmut)
@@ -176,8 +173,7 @@ def main(args=None):
     if best_k is None:
         best_k = len(gen_pat)
     if best_k != len(gen_pat):
-        contextD, gen_pat = downsize_contextD(contextD, gen_pat, best_k)
-        contextD = {key: tuple(v) for key, v in contextD.items()}
+        contextD, gen_pat = contextD.downsized(gen_pat, best_k)
 
     my = n_mut / (n_mut + n_unmut)
     best_beta = (best_alpha * (1.0 - my)) / my
@@ -190,7 +186,7 @@ def main(args=None):
         best_score, M, U, names = bottum_up_array_w_numba.pattern_partition_bottom_up(
             gen_pat, contextD, best_alpha, best_beta, best_penalty, args, n_mut, n_unmut)
 
-    counts = [get_M_U(pat, contextD) for pat in names]
+    counts = contextD.pattern_counts(names)  # get_M_U per pattern (cli.py:287)
     # partition sanity checks of the reference (cli.py:289-292)
     assert M == n_mut
     assert U == n_unmut

@@ -38,6 +38,7 @@
 #include "kp_core.h"
 #include "kp_dp_kernel.h"
 #include "kp_folds.h"
+#include "kp_io.h"
 #include "kp_plan.h"
 
 
@@ -955,5 +956,47 @@ int kp_fold_split(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uin
     *mt_pos = rng.pos;
     return KP_OK;
 }
+
+// ---- k-mer count files (host code) ----
+struct kp_kmer_table {
+    kpio::table t;
+};
+
+int kp_kmer_parse(const char *text, uint64_t nbytes, int columns, const char *super_pattern, int length,
+                  kp_kmer_table **out) {
+    if (!out || (nbytes && !text)) return fail(KP_E_ARG, "bad arguments");
+    *out = nullptr;
+    kp_kmer_table *t = new kp_kmer_table();
+    const std::string err = kpio::parse(text, nbytes, columns, super_pattern, length, t->t);
+    if (!err.empty()) {
+        delete t;
+        return fail(KP_E_ARG, err);
+    }
+    *out = t;
+    return KP_OK;
+}
+
+int kp_kmer_table_info(const kp_kmer_table *t, uint64_t *n, int32_t *k, int64_t *total0, int64_t *total1) {
+    if (!t || !n || !k || !total0 || !total1) return fail(KP_E_ARG, "null argument");
+    *n = t->t.code.size();
+    *k = t->t.k;
+    *total0 = t->t.total0;
+    *total1 = t->t.total1;
+    return KP_OK;
+}
+
+int kp_kmer_table_copy(const kp_kmer_table *t, uint64_t *codes, int64_t *c0, int64_t *c1) {
+    if (!t) return fail(KP_E_ARG, "null table");
+    const size_t n = t->t.code.size();
+    if (n && (!codes || !c0 || !c1)) return fail(KP_E_ARG, "null output");
+    if (n) {
+        memcpy(codes, t->t.code.data(), n * sizeof(uint64_t));
+        memcpy(c0, t->t.c0.data(), n * sizeof(int64_t));
+        memcpy(c1, t->t.c1.data(), n * sizeof(int64_t));
+    }
+    return KP_OK;
+}
+
+void kp_kmer_table_free(kp_kmer_table *t) { delete t; }
 
 }  // extern "C"

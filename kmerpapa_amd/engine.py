@@ -58,7 +58,8 @@ class KPPassStats(ctypes.Structure):
 
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
            "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_pass", "kp_last_pass_stats",
-           "kp_fit_leaves", "kp_dump_lane", "kp_fold_split"]
+           "kp_fit_leaves", "kp_dump_lane", "kp_fold_split", "kp_kmer_parse", "kp_kmer_table_info",
+           "kp_kmer_table_copy", "kp_kmer_table_free"]
 
 
 def load():
@@ -83,6 +84,13 @@ def load():
         L.kp_plan_destroy.argtypes = [vp]
         L.kp_plan_destroy.restype = None
         L.kp_plan_get_info.argtypes = [vp, ctypes.POINTER(KPPlanInfo)]
+        L.kp_kmer_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                    ctypes.POINTER(vp)]
+        L.kp_kmer_table_info.argtypes = [vp, u64p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
+                                         ctypes.POINTER(ctypes.c_int64)]
+        L.kp_kmer_table_copy.argtypes = [vp, vp, vp, vp]
+        L.kp_kmer_table_free.argtypes = [vp]
+        L.kp_kmer_table_free.restype = None
         L.kp_set_counts.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
         L.kp_pass.argtypes = [vp, ctypes.POINTER(KPGroup), ctypes.c_int, vp, vp, vp]
         L.kp_last_pass_stats.argtypes = [vp, ctypes.POINTER(KPPassStats)]
@@ -90,7 +98,7 @@ def load():
         L.kp_dump_lane.argtypes = [vp, ctypes.c_uint32, vp, vp]
         L.kp_fold_split.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_int, vp]
         for name in EXPORTS:
-            if name not in ("kp_destroy", "kp_plan_destroy", "kp_last_error"):
+            if name not in ("kp_destroy", "kp_plan_destroy", "kp_last_error", "kp_kmer_table_free"):
                 getattr(L, name).restype = ctypes.c_int
         _lib = L
         return L
@@ -112,9 +120,8 @@ def kernel_tag():
     h = hashlib.sha1()
     src = os.path.join(_HERE, "csrc")
     for name in ("kp_core.h", "kp_dp_kernel.h", "kp_plan.h"):
-        if True:
-            with open(os.path.join(src, name), "rb") as f:
-                h.update(name.encode() + b"\0" + f.read())
+        with open(os.path.join(src, name), "rb") as f:
+            h.update(name.encode() + b"\0" + f.read())
     return h.hexdigest()[:12]
 
 
@@ -134,6 +141,33 @@ def fold_split(colors, n_folds, prng):
                            _ptr(out)))
     prng.set_state((st[0], key, pos.value, st[3], st[4]))
     return out
+
+
+def parse_kmer_counts(text, columns, super_pattern=None, length=0):
+    """Parse k-mer count text with the native reader (``kp_kmer_parse``, C++).
+
+    ``text``: bytes of a "kmer count" (``columns=2``) or "kmer positive background"
+    (``columns=3``) file.  Returns ``(k, codes uint64, c0 int64, c1 int64, total0,
+    total1)`` with codes sorted (2 bits per letter, first letter most significant).
+    Input errors raise ``ValueError`` with the parser's message."""
+    L = load()
+    buf = bytes(text)
+    t = ctypes.c_void_p()
+    sp = super_pattern.encode("ascii") if super_pattern else None
+    rc = L.kp_kmer_parse(buf, ctypes.c_uint64(len(buf)), int(columns), sp, int(length or 0), ctypes.byref(t))
+    if rc != 0:
+        raise ValueError(L.kp_last_error().decode(errors="replace"))
+    try:
+        n, k = ctypes.c_uint64(), ctypes.c_int32()
+        t0, t1 = ctypes.c_int64(), ctypes.c_int64()
+        _check(L.kp_kmer_table_info(t, ctypes.byref(n), ctypes.byref(k), ctypes.byref(t0), ctypes.byref(t1)))
+        codes = np.zeros(n.value, np.uint64)
+        c0 = np.zeros(n.value, np.int64)
+        c1 = np.zeros(n.value, np.int64)
+        _check(L.kp_kmer_table_copy(t, _ptr(codes), _ptr(c0), _ptr(c1)))
+    finally:
+        L.kp_kmer_table_free(t)
+    return k.value, codes, c0, c1, t0.value, t1.value
 
 
 def device_count():
@@ -274,11 +308,18 @@ class Plan:
 # ----------------------------------------------------------------------------
 
 def kmer_order(gen_pat, contexts):
-    """KmerEnumeration index of every k-mer string in ``contexts`` (vectorised)."""
+    """KmerEnumeration index of every k-mer in ``contexts`` (vectorised): a list of k-mer
+    strings, or a table with ``letters()`` (io_utils.KmerCounts, native parser output)."""
     k = len(gen_pat)
-    if not contexts:
+    if hasattr(contexts, "letters"):
+        raw, name = contexts.letters(), contexts.kmer_at
+    elif not contexts:
         return np.zeros(0, np.int64)
-    raw = np.frombuffer("".join(contexts).encode("ascii"), dtype=np.uint8).reshape(len(contexts), k)
+    else:
+        raw = np.frombuffer("".join(contexts).encode("ascii"), dtype=np.uint8).reshape(len(contexts), k)
+        name = contexts.__getitem__
+    if raw.shape[0] == 0:
+        return np.zeros(0, np.int64)
     idx = np.zeros(len(contexts), np.int64)
     w = 1
     for i, g in enumerate(gen_pat):
@@ -287,7 +328,7 @@ def kmer_order(gen_pat, contexts):
             lut[ord(nuc)] = d
         dig = lut[raw[:, i]]
         if (dig < 0).any():
-            bad = contexts[int(np.argmax(dig < 0))]
+            bad = name(int(np.argmax(dig < 0)))
             raise ValueError(f"k-mer {bad} does not match general pattern {gen_pat}")
         idx += dig * w
         w *= len(code_no[g])
@@ -300,7 +341,7 @@ def counts_in_kmer_order(gen_pat, contexts, M, U, n_kmers, itype):
     nf = 1 if M.ndim == 1 else M.shape[1]
     outM = np.zeros((n_kmers, nf), dtype=itype)
     outU = np.zeros((n_kmers, nf), dtype=itype)
-    idx = kmer_order(gen_pat, list(contexts))
+    idx = kmer_order(gen_pat, contexts if hasattr(contexts, "letters") else list(contexts))
     outM[idx] = np.asarray(M, dtype=itype).reshape(len(idx), nf)
     outU[idx] = np.asarray(U, dtype=itype).reshape(len(idx), nf)
     return outM, outU

@@ -32,6 +32,18 @@ def write_count_files(k, directory):
     return tuple(paths)
 
 
+def write_joint_file(k, directory):
+    """The "kmer positive background" file make_golden.py's cli5b job writes (background
+    file order, positive = 0 where the k-mer has no positive line)."""
+    d = golden_npz("test_data.npz")
+    pos = {str(a): int(b) for a, b in zip(d[f"mutated{k}_kmers"], d[f"mutated{k}_counts"])}
+    p = os.path.join(directory, f"joint_{k}mers.txt")
+    with open(p, "w") as fh:
+        for kmer, c in zip(d[f"background{k}_kmers"], d[f"background{k}_counts"]):
+            fh.write(f"{kmer} {pos.get(str(kmer), 0)} {int(c)}\n")
+    return p
+
+
 def context_table(k):
     """contextD as cli.main builds it (read_input + zero fill), plus gen_pat and totals."""
     from kmerpapa_amd.io_utils import read_postive_and_other

@@ -11,7 +11,7 @@ only numbers it produced.
 Canonical interpreter: /opt/conda/bin/python3.9 (numpy 1.26, scipy 1.7) which follows
 the numpy<2 promotion rules of the reference's pinned numpy 1.23.3.
 
-Usage:  python3 tests/golden/make_golden.py [--jobs small,grid5,fit5,cli5,fit7,cv7,allk5]
+Usage:  python3 tests/golden/make_golden.py [--jobs small,grid5,fit5,cli5,cli5b,fit7,cv7,allk5]
 The GPU box never runs this file (no /root/reference there).
 """
 import argparse
@@ -337,6 +337,56 @@ def job_cli5(out):
             res[name] = {"argv": argv, "rc": rc, "output": open(o).read(),
                          "cvfile": open(f).read(), "stderr": err.getvalue()}
     with open(os.path.join(out, "cli5.json"), "w") as fh:
+        json.dump(res, fh)
+
+
+def _joint_lines(pos_counts, bg_counts):
+    """"kmer positive background" lines (read_joint_kmer_counts format) in background order."""
+    return "".join(f"{x} {pos_counts.get(x, 0)} {c}\n" for x, c in bg_counts.items())
+
+
+def job_cli5b(out):
+    """CLI input variants and --test_smaller_k on the 5-mer data (ref cli.py:118-318,
+    io_utils.py:3-217): joint count file, --negative file, CV over k = 5 and 3.
+
+    The k = 3 lattice (675 cells) is small enough that the CV module's np.empty arrays
+    (CV :93-102) come from recycled heap memory, and its fold totals sum those rows
+    (CV :134-137): the reference's own k = 3 numbers then depend on the heap (a fresh
+    process gives 1328534.5, after the k = 5 pass 1328536.125).  The vectors pin the
+    zero-initialised arrays the reference gets for every large lattice (SURVEY.md 8(a)
+    a3 quirk iii): np.empty is zeros in the CV module for this job."""
+    import io as _io
+    import contextlib
+    import types
+    import numpy as np
+    import kmerpapa.algorithms.bottum_up_array_penalty_plus_pseudo_CV as cvm
+    np_zeroed = types.ModuleType("numpy_zeroed_empty")
+    np_zeroed.__dict__.update(np.__dict__)
+    np_zeroed.empty = np.zeros
+    cvm.np = np_zeroed
+    from kmerpapa import cli
+    pos = os.path.join(REF_DATA, "mutated_5mers.txt")
+    bg = os.path.join(REF_DATA, "background_5mers.txt")
+    res = {}
+    with tempfile.TemporaryDirectory() as td:
+        joint = os.path.join(td, "joint_5mers.txt")
+        with open(joint, "w") as fh:
+            fh.write(_joint_lines(_read_counts("mutated_5mers.txt"), _read_counts("background_5mers.txt")))
+        runs = {
+            "smaller_k": ["-p", pos, "-b", bg, "-c", "3", "5", "-a", "1", "--nfolds", "2", "--seed", "3",
+                          "--test_smaller_k"],
+            "joint": ["-j", joint, "-c", "3", "-a", "0.5"],
+            "negative": ["-p", pos, "-n", bg, "-c", "4", "-a", "1"],
+        }
+        for name, argv in runs.items():
+            o = os.path.join(td, name + ".out")
+            f = os.path.join(td, name + ".cv")
+            err = _io.StringIO()
+            with contextlib.redirect_stderr(err):
+                rc = cli.main(argv + ["-o", o, "-f", f])
+            res[name] = {"argv": argv, "rc": rc, "output": open(o).read(),
+                         "cvfile": open(f).read(), "stderr": err.getvalue()}
+    with open(os.path.join(out, "cli5b.json"), "w") as fh:
         json.dump(res, fh)
 
 

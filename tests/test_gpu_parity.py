@@ -9,7 +9,7 @@ import random
 import numpy as np
 import pytest
 
-from tests.fixtures import bits_equal, context_table, golden_json, golden_npz, write_count_files
+from tests.fixtures import bits_equal, context_table, golden_json, golden_npz, write_count_files, write_joint_file
 
 pytestmark = pytest.mark.gpu
 
@@ -156,6 +156,27 @@ def test_cli5_output_text(eng, run, tmp_path, capsys):
     argv = []
     for a in g["argv"]:
         argv.append(pos if a.endswith("mutated_5mers.txt") else bg if a.endswith("background_5mers.txt") else a)
+    out = tmp_path / "o.txt"
+    cvf = tmp_path / "cv.txt"
+    rc = cli.main(argv + ["-o", str(out), "-f", str(cvf)])
+    assert rc == g["rc"]
+    assert out.read_text() == g["output"]
+    assert cvf.read_text() == g["cvfile"]
+
+
+@pytest.mark.parametrize("run", ["smaller_k", "joint", "negative"])
+def test_cli5b_input_variants(eng, run, tmp_path):
+    """--test_smaller_k CV (k = 5 and 3), a joint count file and a --negative file through
+    the CLI (native reader, array-backed table): output table and CVfile byte-identical to
+    the reference's (golden cli5b.json)."""
+    from kmerpapa_amd import cli
+    g = golden_json("cli5b.json")[run]
+    pos, bg = write_count_files(5, str(tmp_path))
+    joint = write_joint_file(5, str(tmp_path))
+    argv = []
+    for a in g["argv"]:
+        argv.append(pos if a.endswith("mutated_5mers.txt") else bg if a.endswith("background_5mers.txt")
+                    else joint if a.endswith("joint_5mers.txt") else a)
     out = tmp_path / "o.txt"
     cvf = tmp_path / "cv.txt"
     rc = cli.main(argv + ["-o", str(out), "-f", str(cvf)])
