@@ -119,10 +119,11 @@ def _f64_sum(values):
 def _distributed_runner():
     """Under torch.distributed (one process per GPU, e.g. torchrun), each rank runs its
     chunk of the groups on GPU LOCAL_RANK and the root scalars are all-gathered
-    (kmerpapa_amd.shard); otherwise every visible GPU of this process is used."""
+    (kmerpapa_amd.shard); otherwise every visible GPU of this process is used.  torch is
+    not imported here: a caller that set up a process group has imported it already."""
     try:
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        dist = sys.modules.get("torch.distributed")
+        if dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             import os
             from ..shard import sharded_run_groups, torch_all_gather
             local = int(os.environ.get("LOCAL_RANK", "0"))
