@@ -15,7 +15,6 @@ from . import __version__
 from .algorithms import all_kmers_CV, bottum_up_array_penalty_plus_pseudo_CV, bottum_up_array_w_numba
 from .io_utils import read_input_table
 from .papa import Pattern
-from .pattern_utils import matches
 from .score_utils import get_loss
 
 
@@ -180,13 +179,13 @@ def main(args=None):
     if verbose:
         print(f"Training on whole data set with k={best_k} alpha={best_alpha} penalty={best_penalty}",
               file=sys.stderr)
-    if args.score == "all_kmers":  # every k-mer is its own pattern (cli.py:266-271)
-        best_score, M, U, names = 0, n_mut, n_unmut, list(matches(gen_pat))
+    if args.score == "all_kmers":  # every k-mer is its own pattern, matches() order (cli.py:266-271)
+        names, Ms, Us = contextD.match_rows(gen_pat)
+        best_score, M, U, counts = 0, n_mut, n_unmut, list(zip(Ms, Us))
     else:
         best_score, M, U, names = bottum_up_array_w_numba.pattern_partition_bottom_up(
             gen_pat, contextD, best_alpha, best_beta, best_penalty, args, n_mut, n_unmut)
-
-    counts = contextD.pattern_counts(names)  # get_M_U per pattern (cli.py:287)
+        counts = contextD.pattern_counts(names)  # get_M_U per pattern (cli.py:287)
     # partition sanity checks of the reference (cli.py:289-292)
     assert M == n_mut
     assert U == n_unmut
@@ -204,10 +203,10 @@ def main(args=None):
         print("pattern", "p_neg", "p_pos", "p_rate", file=out)
     for pat, (Mp, Up) in zip(names, counts):
         p = (Mp + best_alpha) / (Mp + Up + best_alpha + best_beta)
-        if args.long_output:
-            for context in matches(pat):
-                nm, ns = contextD[context]
-                print(context, ns, nm, float(nm) / (nm + ns), pat, Up, Mp, p, file=out)
+        if args.long_output:  # one row per k-mer of the pattern, matches() order (cli.py:305-311)
+            tail = f" {pat} {Up} {Mp} {p}\n"
+            rows = ([pat], [Mp], [Up]) if len(names) == len(contextD) else contextD.match_rows(pat)
+            out.write("".join(f"{context} {ns} {nm} {float(nm) / (nm + ns)}{tail}" for context, nm, ns in zip(*rows)))
         else:
             print(pat, Up, Mp, p, file=out)
     return 0

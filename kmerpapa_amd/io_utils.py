@@ -257,6 +257,17 @@ class KmerCounts(Mapping):
         U = np.add.reduceat(self.U[order], first)
         return KmerCounts(length, sub[first], M, U), general_pattern[lo:lo + length]
 
+    def match_rows(self, pattern):
+        """(k-mers, positive counts, negative counts) of every k-mer matching ``pattern``, in
+        :func:`matches` order (position 0 fastest), as Python lists."""
+        codes = np.zeros(1, np.uint64)
+        for i in range(len(pattern) - 1, -1, -1):  # position 0 innermost = fastest
+            bases = np.array(["ACGT".index(c) for c in _code[pattern[i]]], np.uint64)
+            codes = (codes[:, None] + bases[None, :] * np.uint64(4 ** (len(pattern) - 1 - i))).reshape(-1)
+        idx = np.searchsorted(self.codes, codes)
+        sub = KmerCounts(self.k, codes, self.M[idx], self.U[idx])
+        return sub._key_list(), sub.M.tolist(), sub.U.tolist()
+
     def pattern_counts(self, patterns):
         """get_M_U (pattern_utils.py:192-215) for many patterns: summed (M, U) of the
         k-mers each pattern matches (every one must be in the table)."""

@@ -185,3 +185,17 @@ def test_reference_test_data_tables(tmp_path):
         assert got[0].lca_pattern() == gp == "NNMNN"
         full = got[0].zero_filled(gp)
         assert len(full) == 512 and full.pattern_counts([gp]) == [get_M_U(gp, dict(full.items()))]
+
+
+def test_match_rows_order():
+    """KmerCounts.match_rows: the k-mers of a pattern in matches() order (position 0
+    fastest) with their counts, as the long output walks them (cli.py:305-311)."""
+    rng = np.random.RandomState(1)
+    gp = "NMRS"
+    D = {k: (int(rng.randint(0, 9)), int(rng.randint(1, 99))) for k in matches(gp)}
+    codes = np.array([int("".join(str("ACGT".index(c)) for c in k), 4) for k in sorted(D)], np.uint64)
+    T = io_utils.KmerCounts(4, codes, [D[k][0] for k in sorted(D)], [D[k][1] for k in sorted(D)])
+    for pat in ["NMRS", "ACRS", "NAGS", "TMGC"]:
+        ks, m, u = T.match_rows(pat)
+        assert ks == list(matches(pat))
+        assert m == [D[x][0] for x in ks] and u == [D[x][1] for x in ks]
