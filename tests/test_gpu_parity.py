@@ -279,3 +279,44 @@ def test_random_patterns_vs_oracle(eng, seed):
             assert bits_equal(score, ref["score"][:, f]), (gp, c, f)
             assert bits_equal(re[lane], ref["root_test"][f])
     plan.close()
+
+
+@pytest.mark.parametrize("seed", range(10, 14))
+def test_random_6mers_vs_oracle(eng, seed):
+    """Random 6-position general patterns (at most two N), 1-8 penalties per group and
+    block sizes 0 (default), 128 and 1024 cells: every cell's float32 score and every
+    root test value equal the oracle's, bit for bit."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality, matches
+    from oracle import oracle as O
+    rng = random.Random(seed)
+    codes = list("MRSWKYACGTBDHV")
+    gp = "".join(rng.choice(codes) for _ in range(6))
+    for i in rng.sample(range(6), 2):
+        gp = gp[:i] + "N" + gp[i + 1:]
+    ctx = {}
+    for kmer in matches(gp):
+        bg = rng.randrange(0, 20000) if rng.random() > 0.05 else 0
+        pos = rng.randrange(0, bg + 1) // rng.choice([1, 10, 100])
+        ctx[kmer] = (pos, bg - pos)
+    nf = rng.choice([2, 4])
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(seed), np.uint32)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    alpha = rng.choice([0.3, 1.0, 4.0])
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr = tot_m.sum() - tot_m
+    utr = tot_u.sum() - tot_u
+    betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+    pens = sorted(rng.sample([0.0, 1.0, 2.5, 4.0, 5.5, 7.0, 9.0, 12.0], rng.randint(1, 8)))
+    plan = eng.Plan(eng.get_device(0), gp, rng.choice([0, 128, 1024]))
+    plan.set_counts(Mk, Uk)
+    rt, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
+    for pi, c in enumerate(pens):
+        ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 32)
+        for f in range(nf):
+            lane = f * len(pens) + pi
+            score, _ = plan.dump_lane(lane)
+            assert bits_equal(score, ref["score"][:, f]), (gp, c, f)
+            assert bits_equal(re[lane], ref["root_test"][f])
+    plan.close()
