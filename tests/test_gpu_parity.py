@@ -320,3 +320,36 @@ def test_random_6mers_vs_oracle(eng, seed):
             assert bits_equal(score, ref["score"][:, f]), (gp, c, f)
             assert bits_equal(re[lane], ref["root_test"][f])
     plan.close()
+
+
+@pytest.mark.parametrize("gp", ["ACG", "AMG", "N", "MA", "TTNTT", "RYSWKM"])
+def test_degenerate_lattices_fit_vs_oracle(eng, gp):
+    """Edge lattices: a single cell (no ambiguous position), one ambiguous position, a
+    1-mer, all-binary codes, zero counts: the fit (score, counts, partition and order)
+    equals the oracle's."""
+    from kmerpapa_amd.algorithms import bottum_up_array_w_numba as fitm
+    from kmerpapa_amd.pattern_utils import matches
+    from oracle import oracle as O
+    rng = random.Random(len(gp) * 31 + ord(gp[0]))
+    ctx = {}
+    for kmer in matches(gp):
+        bg = rng.randrange(0, 5000) if rng.random() > 0.2 else 0
+        pos = rng.randrange(0, bg + 1) // 50
+        ctx[kmer] = (pos, bg - pos)
+    if all(v == (0, 0) for v in ctx.values()):
+        ctx[next(iter(ctx))] = (3, 1000)
+    nm = sum(v[0] for v in ctx.values())
+    nu = sum(v[1] for v in ctx.values())
+    my = nm / (nm + nu)
+    alpha, pen = 0.5, 3.0
+    beta = (alpha * (1.0 - my)) / my
+
+    class A:
+        verbosity = 0
+    sc, Mr, Ur, names = fitm.pattern_partition_bottom_up(gp, ctx, alpha, beta, pen, A, nm, nu)
+    M = np.array([ctx[k][0] for k in ctx], np.int64)
+    U = np.array([ctx[k][1] for k in ctx], np.int64)
+    rs, rm, ru, rnames, _ = O.fit(gp, list(ctx), M, U, alpha, beta, pen, 32)
+    assert np.float32(sc).tobytes() == np.float32(rs).tobytes()
+    assert (int(Mr), int(Ur)) == (rm, ru)
+    assert names == rnames
