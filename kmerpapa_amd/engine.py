@@ -405,6 +405,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     Returns ``(root_train, root_test, n_leaves)`` arrays over all lanes, group-major.
     """
     devices = list(devices) if devices is not None else visible_devices()[:1]
+    devices = list(dict.fromkeys(devices))  # one host thread per GPU: a device's plan is not shared
     if not devices:
         raise KPError(-3, "no GPU visible")
     from .shard import chunk_bounds
