@@ -7,6 +7,7 @@
 // (PatternEnumeration, pattern_utils.py:247-266).
 #pragma once
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -277,8 +278,53 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     for (int s = 0; s <= hmax; ++s) P.hoff[s + 1] += P.hoff[s];
     P.hlist.resize(g.nblocks);
     {
+        // Block order inside a level = the order the sweep kernel runs them in, which sets
+        // how often a child row read by several parents is still in L2 / the Infinity Cache.
+        // Parents of one child differ in one high position, so the positions that vary
+        // fastest get their reuse: those with the most split pairs (largest radix) go
+        // first, later positions before earlier ones (measured: random order +25 % time,
+        // ascending h (position t fastest) +1 %, this order the best of those tried;
+        // DESIGN.md §5).  KP_BLOCK_PERM="5-4-..." (high positions, fastest first) and
+        // KP_BLOCK_ORDER=1 (shuffled) override it for experiments.
+        std::vector<int> perm;
+        if (const char *pe = getenv("KP_BLOCK_PERM")) {  // digits separated by any non-digit
+            for (const char *c = pe; *c;) {
+                const int v = atoi(c);
+                if (v >= 0 && v < g.kh && std::find(perm.begin(), perm.end(), v) == perm.end()) perm.push_back(v);
+                while (*c >= '0' && *c <= '9') ++c;
+                while (*c && (*c < '0' || *c > '9')) ++c;
+            }
+        } else {
+            for (int i = g.kh - 1; i >= 0; --i) perm.push_back(i);
+            std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return g.r[g.t + a] > g.r[g.t + b]; });
+        }
+        for (int i = g.kh - 1; i >= 0; --i)  // complete a partial explicit permutation
+            if (std::find(perm.begin(), perm.end(), i) == perm.end()) perm.push_back(i);
         std::vector<uint64_t> fill(P.hoff.begin(), P.hoff.end() - 1);
-        for (uint64_t h = 0; h < g.nblocks; ++h) P.hlist[fill[hl[h]]++] = (uint32_t)h;
+        std::vector<uint32_t> dig(g.kh, 0);
+        uint64_t h = 0;
+        for (uint64_t n = 0; n < g.nblocks; ++n) {  // mixed-radix counter, perm[0] fastest
+            P.hlist[fill[hl[h]]++] = (uint32_t)h;
+            for (int j = 0; j < g.kh; ++j) {
+                const int i = perm[j];
+                if (++dig[i] < g.r[g.t + i]) {
+                    h += g.hcg[i];
+                    break;
+                }
+                h -= (uint64_t)(dig[i] - 1) * g.hcg[i];
+                dig[i] = 0;
+            }
+        }
+        const char *bo = getenv("KP_BLOCK_ORDER");
+        if (bo && atoi(bo) == 1)
+            for (int s = 0; s <= hmax; ++s) {  // experiment: shuffled (no reuse order)
+                uint32_t *b = P.hlist.data() + P.hoff[s], *e = P.hlist.data() + P.hoff[s + 1];
+                uint64_t x = 0x9E3779B97F4A7C15ull + (uint64_t)s;
+                for (uint32_t *q = e; q - b > 1; --q) {
+                    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                    std::swap(q[-1], b[x % (uint64_t)(q - b)]);
+                }
+            }
     }
     if (g.kh > 15) return "too many high positions for packed digits";
     P.hdig.resize(g.nblocks);
