@@ -40,7 +40,8 @@ struct kp_dp_params {
     int lmax;
     uint32_t ptab_entries;     // separable count table entries (kp_plan.h)
     uint32_t pscratch_entries; // largest intermediate table of its build
-    int remap;  // 1 = XCD-contiguous block order (KP_XCD_REMAP=1; measured 4% slower, off by default)
+    int remap;  // block -> XCD mapping: G > 1 = runs of G list entries per XCD (default 8),
+                // 1 = XCD-contiguous (7 % slower), 0 = hardware round-robin
     int lanesplit;  // split a cell's lanes over threads on narrow levels (KP_LANE_SPLIT=0 disables)
     unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
     int dbg;  // timing ablation only (KP_DEBUG_SKIP, wrong results): 1 = skip gather, 2 = skip level phase,
@@ -153,9 +154,15 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     const unsigned long long st_real0 = __builtin_amdgcn_s_memrealtime(), st_t0 = st_prev;
 #endif
     uint32_t widx = blockIdx.x;
-    if (P.remap) {  // XCD-contiguous runs of the level's block list (A/B option)
+    if (P.remap == 1) {  // XCD-contiguous runs of the level's block list (A/B option)
         const uint32_t nb = gridDim.x, q = nb >> 3, r = nb & 7u, x = blockIdx.x & 7u;
         widx = x * q + (x < r ? x : r) + (blockIdx.x >> 3);
+    } else if (P.remap > 1) {  // runs of G = remap consecutive list entries per XCD (A/B option)
+        const uint32_t G = (uint32_t)P.remap, full = gridDim.x / (8 * G) * (8 * G);
+        if (blockIdx.x < full) {
+            const uint32_t x = blockIdx.x & 7u, sl = blockIdx.x >> 3;
+            widx = ((sl / G) * 8 + x) * G + sl % G;
+        }
     }
     const uint64_t h = P.T.hlist[P.hbase + widx];
     const kp_group_dev *G = P.groups + blockIdx.y;
