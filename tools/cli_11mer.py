@@ -7,6 +7,7 @@ import json
 import os
 import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -15,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
-out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "cli11")
+out = sys.argv[1] if len(sys.argv) > 1 else tempfile.mkdtemp(prefix="kp_cli_")  # large inputs: not under gpurun_out
 os.makedirs(out, exist_ok=True)
 t0 = time.time()
 kmers, M, U = bench.synthetic_counts("NNNNNMNNNNN")

@@ -5,13 +5,14 @@ import json
 import os
 import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
-out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out", "cli9")
+out = sys.argv[1] if len(sys.argv) > 1 else tempfile.mkdtemp(prefix="kp_cli_")  # large inputs: not under gpurun_out
 os.makedirs(out, exist_ok=True)
 kmers, M, U = bench.synthetic_counts("NNNNMNNNN")
 with open(os.path.join(out, "pos.txt"), "w") as f:
