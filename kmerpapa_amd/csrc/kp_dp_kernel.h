@@ -23,7 +23,6 @@ struct kp_dev_tables {
     const uint16_t *kllist;
     const uint32_t *hlist;
     const kp_lowdesc *ldesc;
-    const uint64_t *pw;
     const uint64_t *hdig;
     const uint8_t *lowmask;
     const uint4 *lpairs;  // low split-pair lists in 4-pair chunks (kp_plan.h lpairs)
@@ -174,15 +173,14 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
 #pragma unroll
     for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
 
-    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | pw[t][16] | lm[t][16]
+    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | lm[t][16]
     //      (count-table scratch aliases st, which the gather fills afterwards; every carve
     //       offset is a multiple of 16 bytes)
     const size_t st_bytes = (size_t)NL * Bpad * 4, scr_bytes = (size_t)P.pscratch_entries * 4 * sizeof(CT);
     float *st = reinterpret_cast<float *>(smem);
     CT *ptab = reinterpret_cast<CT *>(smem + (st_bytes > scr_bytes ? st_bytes : ((scr_bytes + 15) & ~(size_t)15)));
     kp_hpair *hp = reinterpret_cast<kp_hpair *>(ptab + (((size_t)P.ptab_entries * 2 + 3) & ~(size_t)3));
-    uint64_t *pw = reinterpret_cast<uint64_t *>(hp + (g.kh * 7 + 1));
-    uint8_t *lm = reinterpret_cast<uint8_t *>(pw + g.t * 16);
+    uint8_t *lm = reinterpret_cast<uint8_t *>(hp + (g.kh * 7 + 1));
 #ifdef KP_STAMPS
     unsigned long long *st_lds = reinterpret_cast<unsigned long long *>(lm + ((g.t * 16 + 15) & ~15));
     if (threadIdx.x < 32) st_lds[threadIdx.x] = 0;
@@ -211,8 +209,6 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         hp[p].h2 = (h - (uint64_t)(d - T.pb[d][rem]) * g.hcg[i]) * rowstride;  // offsets of lane 0
         hp[p].code = (uint32_t)(((g.t + i) << 3) | rem);
     }
-    for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 32u; e += blockDim.x)
-        reinterpret_cast<uint32_t *>(pw)[e] = reinterpret_cast<const uint32_t *>(P.T.pw)[e];
     for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 16u; e += blockDim.x) lm[e] = P.T.lowmask[e];
     __syncthreads();  // lm is read by every thread below
 

@@ -371,7 +371,6 @@ struct kp_plan {
     uint16_t *d_kllist = nullptr;
     uint32_t *d_hlist = nullptr;
     kp_lowdesc *d_ldesc = nullptr;
-    uint64_t *d_pw = nullptr;
     uint64_t *d_hdig = nullptr;
     uint8_t *d_lowmask = nullptr;
     uint32_t *d_lpairs = nullptr;
@@ -408,7 +407,6 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     T.kllist = p->d_kllist;
     T.hlist = p->d_hlist;
     T.ldesc = p->d_ldesc;
-    T.pw = p->d_pw;
     T.hdig = p->d_hdig;
     T.lowmask = p->d_lowmask;
     T.lpairs = reinterpret_cast<const uint4 *>(p->d_lpairs);
@@ -490,7 +488,7 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
     if ((rc = upload(&p->d_tabs, p->hp.tabs)) || (rc = upload(&p->d_lowinfo, p->hp.lowinfo)) ||
         (rc = upload(&p->d_loff, p->hp.loff)) || (rc = upload(&p->d_klofs, p->hp.klofs)) ||
         (rc = upload(&p->d_kllist, p->hp.kllist)) || (rc = upload(&p->d_hlist, p->hp.hlist)) ||
-        (rc = upload(&p->d_ldesc, p->hp.ldesc)) || (rc = upload(&p->d_pw, p->hp.pw)) ||
+        (rc = upload(&p->d_ldesc, p->hp.ldesc)) ||
         (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_lowmask, p->hp.lowmask)) ||
         (rc = upload(&p->d_lpairs, p->hp.lpairs))) {
         kp_plan_destroy(p);
@@ -504,7 +502,7 @@ void kp_plan_destroy(kp_plan *p) {
     if (!p) return;
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
     void *bufs[] = {p->d_tabs,    p->d_lowinfo, p->d_loff,   p->d_klofs,   p->d_kllist, p->d_hlist, p->d_ldesc,
-                    p->d_pw,      p->d_hdig,    p->d_lowmask, p->d_lpairs, p->d_K,      p->d_S,      p->d_nodes, p->d_groups,
+                    p->d_hdig,    p->d_lowmask, p->d_lpairs, p->d_K,      p->d_S,      p->d_nodes, p->d_groups,
                     p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
                     p->d_leaves};
     for (void *b : bufs) dfree(b);
@@ -596,7 +594,7 @@ static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
     const size_t st = (size_t)nl * g.Bpad * 4;
     const size_t scratch = (((size_t)hp.pscratch_entries * 4 * ct_bytes) + 15) & ~(size_t)15;  // 2 build buffers
     const size_t ptab = ((((size_t)hp.ptab_entries * 2 + 3) & ~(size_t)3)) * ct_bytes;
-    return std::max(st, scratch) + ptab + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) + (size_t)g.t * 16 * 8 +
+    return std::max(st, scratch) + ptab + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) +
            (((size_t)g.t * 16 + 15) & ~(size_t)15) + 16
 #ifdef KP_STAMPS
            + 32 * sizeof(unsigned long long)
