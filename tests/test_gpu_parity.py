@@ -353,3 +353,51 @@ def test_degenerate_lattices_fit_vs_oracle(eng, gp):
     assert np.float32(sc).tobytes() == np.float32(rs).tobytes()
     assert (int(Mr), int(Ur)) == (rm, ru)
     assert names == rnames
+
+
+@pytest.mark.parametrize("per_wg", [1, 2, 3, 4, 6, 7, 8])
+def test_lanes_per_workgroup_vs_oracle(eng, per_wg, monkeypatch):
+    """Every lanes-per-workgroup kernel instantiation (KP_LANES_PER_WG; the default is 5)
+    on an 8-penalty group of a small-block 5-mer: all cells equal the oracle's."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    from oracle import oracle as O
+    monkeypatch.setenv("KP_LANES_PER_WG", str(per_wg))
+    rng = random.Random(100 + per_wg)
+    gp, ctx = _random_case(rng, 5)
+    nf = 3
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(per_wg), np.uint32)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    alpha = 1.0
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr = tot_m.sum() - tot_m
+    utr = tot_u.sum() - tot_u
+    betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+    pens = [0.5, 1.5, 2.5, 3.5, 4.5, 6.0, 8.0, 11.0]
+    plan = eng.Plan(eng.get_device(0), gp, 64)
+    plan.set_counts(Mk, Uk)
+    rt, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
+    for pi, c in enumerate(pens):
+        ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 32)
+        for f in range(nf):
+            lane = f * len(pens) + pi
+            score, _ = plan.dump_lane(lane)
+            assert bits_equal(score, ref["score"][:, f]), (gp, per_wg, c, f)
+            assert bits_equal(re[lane], ref["root_test"][f])
+    plan.close()
+
+
+def test_error_paths(eng):
+    """Errors come back as exceptions with the library's message, never as wrong numbers."""
+    dev = eng.get_device(0)
+    plan = eng.Plan(dev, "NMN", 0)
+    with pytest.raises(eng.KPError, match="counts"):
+        plan.run([(0, 1.0, 1.0, [1.0])])  # no counts set
+    with pytest.raises(ValueError):
+        plan.run([(0, 1.0, 1.0, [1.0] * 9)])  # more than 8 penalties in a group
+    plan.close()
+    with pytest.raises(eng.KPError):
+        eng.Plan(dev, "NXN", 0)  # not an IUPAC code
+    with pytest.raises(eng.KPError, match="too many blocks"):
+        eng.Plan(dev, "NNNNNNNNNNNN", 0)  # 15^12 cells: more blocks than 32-bit ids
