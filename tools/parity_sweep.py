@@ -1,0 +1,84 @@
+"""Randomised GPU-vs-oracle parity sweep (not part of the test suite: a longer run of
+tests/test_gpu_parity.py's random cases).  Random IUPAC general patterns (k = 3..6, at
+most two N), random counts (zeros included), folds, pseudo counts, 1-8 penalties, block
+sizes and lanes per workgroup; every cell's float32 score and every root test value must
+equal the oracle's bit for bit.  usage: python tools/parity_sweep.py N_CASES SEED  (SWEEP_MAX_CELLS bounds the lattice)"""
+import os
+import random
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from kmerpapa_amd import engine as eng  # noqa: E402
+from kmerpapa_amd.CV_tools import fold_tables  # noqa: E402
+from kmerpapa_amd.pattern_utils import generality, matches, perm_code  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+
+MAX_CELLS = int(os.environ.get("SWEEP_MAX_CELLS", "300000"))
+
+
+def case(rng):
+    k = rng.choice([3, 4, 5, 6, 7])
+    while True:
+        gp = "".join(rng.choice("MRSWKYACGTBDHVNNN") for _ in range(k))
+        if np.prod([len(perm_code[c]) for c in gp]) <= MAX_CELLS:
+            break
+    ctx = {}
+    for kmer in matches(gp):
+        bg = rng.randrange(0, 30000) if rng.random() > 0.1 else 0
+        pos = rng.randrange(0, bg + 1) // rng.choice([1, 5, 50, 500])
+        ctx[kmer] = (pos, bg - pos)
+    if sum(v[0] for v in ctx.values()) == 0:
+        ctx[next(iter(ctx))] = (5, 100)
+    return gp, ctx
+
+
+def main():
+    n, seed = int(sys.argv[1]), int(sys.argv[2])
+    rng = random.Random(seed)
+    dev = eng.get_device(0)
+    bad = 0
+    t0 = time.time()
+    for i in range(n):
+        gp, ctx = case(rng)
+        nf = rng.choice([2, 3, 5])
+        os.environ["KP_LANES_PER_WG"] = str(rng.choice([1, 2, 3, 4, 5, 5, 5, 6, 8]))
+        contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(i), np.uint32)
+        Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+        alpha = rng.choice([0.0, 0.1, 1.0, 7.0])
+        tot_m = Mf.sum(axis=0).astype(np.uint64)
+        tot_u = Uf.sum(axis=0).astype(np.uint64)
+        mtr, utr = tot_m.sum() - tot_m, tot_u.sum() - tot_u
+        with np.errstate(divide="ignore", invalid="ignore"):
+            betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+        pens = sorted(rng.sample([0.0, 0.7, 2.0, 3.3, 5.0, 8.0, 13.0, 21.0], rng.randint(1, 8)))
+        plan = eng.Plan(dev, gp, rng.choice([0, 0, 16, 64, 512, 2048]))
+        plan.set_counts(Mk, Uk)
+        try:
+            _, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
+            for pi, c in enumerate(pens):
+                ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 32)
+                for f in range(nf):
+                    lane = f * len(pens) + pi
+                    score, _ = plan.dump_lane(lane)
+                    ok = np.array_equal(np.asarray(score).view(np.uint32), ref["score"][:, f].view(np.uint32)) and \
+                        np.float32(re[lane]).tobytes() == np.float32(ref["root_test"][f]).tobytes()
+                    if not ok:
+                        bad += 1
+                        print("MISMATCH", i, gp, nf, alpha, c, f, flush=True)
+        except eng.KPError as e:
+            print("error", i, gp, alpha, e, flush=True)
+            bad += 1
+        plan.close()
+        if i % 20 == 0:
+            print(f"case {i} {gp} ({generality(gp)} k-mers) {bad} bad so far, {time.time() - t0:.0f} s", flush=True)
+    print(f"done: {n} cases, {bad} mismatches", flush=True)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
