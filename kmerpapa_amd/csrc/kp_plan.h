@@ -301,20 +301,58 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
         for (int i = g.kh - 1; i >= 0; --i)  // complete a partial explicit permutation
             if (std::find(perm.begin(), perm.end(), i) == perm.end()) perm.push_back(i);
         std::vector<uint64_t> fill(P.hoff.begin(), P.hoff.end() - 1);
-        std::vector<uint32_t> dig(g.kh, 0);
-        uint64_t h = 0;
-        for (uint64_t n = 0; n < g.nblocks; ++n) {  // mixed-radix counter, perm[0] fastest
-            P.hlist[fill[hl[h]]++] = (uint32_t)h;
-            for (int j = 0; j < g.kh; ++j) {
-                const int i = perm[j];
-                if (++dig[i] < g.r[g.t + i]) {
-                    h += g.hcg[i];
-                    break;
+        // KP_BLOCK_TILE=T (experiment): tiles of T digits per high position, the digits
+        // inside a tile (perm order) varying faster than the tile coordinates
+        const char *te = getenv("KP_BLOCK_TILE");
+        const uint32_t tile = te ? (uint32_t)atoi(te) : 0u;
+        if (tile > 0) {
+            std::vector<uint32_t> tr(g.kh), to(g.kh, 0), ti(g.kh, 0);
+            for (int i = 0; i < g.kh; ++i) tr[i] = (g.r[g.t + i] + tile - 1) / tile;
+            for (;;) {
+                std::fill(ti.begin(), ti.end(), 0u);
+                for (;;) {
+                    bool ok = true;
+                    uint64_t h = 0;
+                    for (int i = 0; i < g.kh; ++i) {
+                        const uint32_t d = to[i] * tile + ti[i];
+                        if (d >= g.r[g.t + i]) { ok = false; break; }
+                        h += (uint64_t)d * g.hcg[i];
+                    }
+                    if (ok) P.hlist[fill[hl[h]]++] = (uint32_t)h;
+                    int j = 0;
+                    for (; j < g.kh; ++j) {
+                        const int i = perm[j];
+                        if (++ti[i] < tile) break;
+                        ti[i] = 0;
+                    }
+                    if (j == g.kh) break;
                 }
-                h -= (uint64_t)(dig[i] - 1) * g.hcg[i];
-                dig[i] = 0;
+                int j = 0;
+                for (; j < g.kh; ++j) {
+                    const int i = perm[j];
+                    if (++to[i] < tr[i]) break;
+                    to[i] = 0;
+                }
+                if (j == g.kh) break;
+            }
+        } else {
+            std::vector<uint32_t> dig(g.kh, 0);
+            uint64_t h = 0;
+            for (uint64_t n = 0; n < g.nblocks; ++n) {  // mixed-radix counter, perm[0] fastest
+                P.hlist[fill[hl[h]]++] = (uint32_t)h;
+                for (int j = 0; j < g.kh; ++j) {
+                    const int i = perm[j];
+                    if (++dig[i] < g.r[g.t + i]) {
+                        h += g.hcg[i];
+                        break;
+                    }
+                    h -= (uint64_t)(dig[i] - 1) * g.hcg[i];
+                    dig[i] = 0;
+                }
             }
         }
+        for (int s = 0; s <= hmax; ++s)
+            if (fill[s] != P.hoff[s + 1]) return "block order does not cover every block";
         const char *bo = getenv("KP_BLOCK_ORDER");
         if (bo && atoi(bo) == 1)
             for (int s = 0; s <= hmax; ++s) {  // experiment: shuffled (no reuse order)
