@@ -42,6 +42,7 @@ struct kp_dp_params {
     int remap;  // block -> XCD mapping: G > 1 = runs of G list entries per XCD (default 8),
                 // 1 = XCD-contiguous (7 % slower), 0 = hardware round-robin
     int lanesplit;  // split a cell's lanes over threads on narrow levels (KP_LANE_SPLIT=0 disables)
+    int ntstore;    // 1 = score rows stored non-temporally (default; KP_NT_STORE=0 for plain stores)
     unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
     int dbg;  // timing ablation only (KP_DEBUG_SKIP, wrong results): 1 = skip gather, 2 = skip level phase,
               // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier
@@ -334,8 +335,14 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
         const uint32_t ll = item / nch, c = item % nch;
         const float *sl = st + (size_t)(4 * c) * NL + ll;
-        *reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c) =
-            make_float4(sl[0], sl[NL], sl[2 * NL], sl[3 * NL]);
+        float4 *dst = reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c);
+        const float4 v = make_float4(sl[0], sl[NL], sl[2 * NL], sl[3 * NL]);
+        if (P.ntstore) {
+            typedef float kp_f4v __attribute__((ext_vector_type(4)));
+            const kp_f4v w = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(w, reinterpret_cast<kp_f4v *>(dst));
+        } else
+            *dst = v;
     }
     KP_STAMP(2);
 #ifdef KP_STAMPS

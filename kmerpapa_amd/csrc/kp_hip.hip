@@ -740,6 +740,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     // XCDs): neighbours in the reuse order share their L2; measured -1 %
     P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 8;
     P.lanesplit = getenv("KP_LANE_SPLIT") ? atoi(getenv("KP_LANE_SPLIT")) : 1;
+    P.ntstore = getenv("KP_NT_STORE") ? atoi(getenv("KP_NT_STORE")) : 1;
     P.stamps = nullptr;
 #ifdef KP_STAMPS
     static unsigned long long *d_stamps = nullptr;
