@@ -15,13 +15,20 @@ reduction use gloo on the host.
 
 Timed region: K steps between two barriers; inputs (fold counts, per-block count tables)
 are resident in HBM before it starts.  Units = cells x lanes, summed over ranks.
-The roofline object prices the DP sweep kernel (kp_dp_kernel): algorithmic bytes per
-SURVEY.md §8d (16 B per split pair, 8 B per cell written, 6 s per aggregated cell, 2 s
-per k-mer, per lane) over the HIP-event duration of its launches; "traffic" is the
-PMC-measured HBM bytes per pass (profiles/, rocprofv3 FETCH_SIZE/WRITE_SIZE with the
-gfx950 x2 FETCH correction) when a matching profile summary is committed.
-The cpu_baseline leg times the CPU oracle (oracle/kp_oracle.c, a single-threaded C
-port of the reference's DP) on a bounded sample of the same counts.
+The roofline object prices the DP sweep kernel (kp_dp_kernel, all launches of one pass)
+against HBM: ``achieved`` = the bytes the blocked sweep must move per pass -- every
+high-position split pair reads two child-block rows (2 x 4 B per unit) and every cell is
+written once (4 B): (8 P_high + 4) B per unit, P_high = split pairs per cell at high
+positions -- over the HIP-event time of the pass's launches.  ``traffic`` is
+the rocprofv3 PMC L2-to-fabric byte count of the same pass (FETCH_SIZE x2 + WRITE_SIZE;
+it includes Infinity-Cache hits, so it is an upper bound on HBM bytes), taken from the
+committed profile whose kernel tag matches this build and launch configuration.  The
+floor (4 B read + 4 B written per unit, every row moved once) and the SURVEY.md 8(d)
+naive per-cell figure (16 B per split pair, ...) are reported beside it.
+The cpu_baseline leg times the CPU oracle (oracle/kp_oracle.c, a C restatement of the
+reference's DP) on a bounded sample of the same counts: the reference's own fan-out
+(README.md:39-51, one process per grid point) as one single-threaded oracle task per
+(alpha, c) on every host core, and one task alone on one core.
 """
 import argparse
 import json
@@ -74,14 +81,30 @@ def synthetic_counts(gen_pat=GEN_PAT, seed=9):
     return kmers, pos.astype(np.int64), (bg - pos).astype(np.int64)
 
 
+def kmer_table(kmers, M, U):
+    """The CLI's array-backed count table (io_utils.KmerCounts, sorted 2-bit codes) of a
+    k-mer list: what the native reader hands the CV driver."""
+    from kmerpapa_amd.io_utils import KmerCounts
+    k = len(kmers[0])
+    raw = np.frombuffer("".join(kmers).encode("ascii"), np.uint8).reshape(len(kmers), k)
+    lut = np.zeros(256, np.uint64)
+    for i, ch in enumerate("ACGT"):
+        lut[ord(ch)] = i
+    codes = np.zeros(len(kmers), np.uint64)
+    for j in range(k):
+        codes = codes * np.uint64(4) + lut[raw[:, j]]
+    o = np.argsort(codes, kind="stable")
+    return KmerCounts(k, codes[o], np.asarray(M, np.int64)[o], np.asarray(U, np.int64)[o])
+
+
 def prepare(gen_pat, seed=1, alphas=ALPHAS, penalties=PENALTIES, nfolds=NFOLDS):
     """Fold split (reference RNG stream) and betas for every (alpha, fold)."""
     kmers, M, U = synthetic_counts(gen_pat)
-    ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
+    table = kmer_table(kmers, M, U)
     total = int(M.sum() + U.sum())
     itype = np.uint64 if total > np.iinfo(np.uint32).max else np.uint32
     t0 = time.time()
-    contexts, Mf, Uf = fold_tables(ctx, nfolds, np.random.RandomState(seed), itype)
+    contexts, Mf, Uf = fold_tables(table, nfolds, np.random.RandomState(seed), itype)
     t_fold = time.time() - t0
     Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, generality(gen_pat), itype)
     msum = Mk.sum(axis=0, dtype=np.uint64)
@@ -93,18 +116,33 @@ def prepare(gen_pat, seed=1, alphas=ALPHAS, penalties=PENALTIES, nfolds=NFOLDS):
         betas = (a * (1.0 - my)) / my
         for f in range(nfolds):
             groups.append((f, a, float(betas[f]), list(penalties)))
-    return {"Mk": Mk, "Uk": Uk, "groups": groups, "itype": itype, "t_fold_s": t_fold, "contexts": contexts,
-            "Mf": Mf, "Uf": Uf, "total": total, "gen_pat": gen_pat, "alphas": list(alphas),
+    return {"Mk": Mk, "Uk": Uk, "groups": groups, "itype": itype, "t_fold_s": t_fold, "contexts": list(table),
+            "ctx": table, "Mf": Mf, "Uf": Uf, "total": total, "gen_pat": gen_pat, "alphas": list(alphas),
             "penalties": list(penalties), "nfolds": nfolds}
 
 
-def cpu_baseline(prep, seconds_hint=15.0):
-    """Time the single-threaded CPU oracle on a bounded sample of the same counts: the
-    sub-lattice with the two outermost ambiguous positions fixed to 'A' (3.4e7 cells),
-    one (alpha, c) over all folds."""
+def host_cores():
+    """Host cores this job may use: $OMP_NUM_THREADS (the GPU box sets its per-GPU CPU
+    share there), else the affinity mask."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline(prep):
+    """Time the CPU oracle on a bounded sample of the same counts: the sub-lattice with the
+    two outermost ambiguous positions fixed to 'A' (3.4e7 cells for the 9-mer), one (alpha, c)
+    over all folds per task.  Tasks run as the reference's README fans a grid out (one
+    independent single-threaded job per (alpha, c)), one per host core, concurrently; one
+    task alone on one core is reported beside it."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
     gp = prep["gen_pat"]
-    # fix the two outermost still-ambiguous positions to A: a 15^6 x 3 = 3.4e7-cell sample
     amb = [i for i, x in enumerate(gp) if x != "A"]
     fixed = {amb[0], amb[-1]}
     sub = "".join("A" if i in fixed else x for i, x in enumerate(gp))
@@ -112,17 +150,32 @@ def cpu_baseline(prep, seconds_hint=15.0):
     ctxs = [prep["contexts"][i] for i in keep]
     Mf = prep["Mf"][keep]
     Uf = prep["Uf"][keep]
-    g = prep["groups"][0]
     nf = prep["nfolds"]
-    betas = [prep["groups"][f][2] for f in range(nf)]
     bits = 8 * np.dtype(prep["itype"]).itemsize
+    tasks = [(g[1], [prep["groups"][a_i * nf + f][2] for f in range(nf)], c)
+             for a_i, g in enumerate(prep["groups"][::nf]) for c in g[3]]
+    O.lib()
+
+    def one(task):
+        a, betas, c = task
+        O.cv_pass(sub, ctxs, Mf, Uf, a, betas, c, bits)  # ctypes drops the GIL: tasks run in parallel
     t0 = time.time()
-    O.cv_pass(sub, ctxs, Mf, Uf, g[1], betas, g[3][0], bits)
-    dt = time.time() - t0
+    one(tasks[0])
+    t1 = time.time() - t0
+    cores = host_cores()
+    # memory: ~4.1 GB per concurrent 9-mer sample task
+    par = max(1, min(cores, len(tasks)))
+    t0 = time.time()
+    with ThreadPoolExecutor(par) as ex:
+        list(ex.map(one, [tasks[i % len(tasks)] for i in range(par)]))
+    tn = time.time() - t0
     units = O.npat(sub) * nf
-    return {"value": units / dt, "unit": "cells*folds*(alpha,c)/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/kp_oracle.c kpo_cv on sub-lattice {sub} of the same counts "
-                      f"({O.npat(sub)} cells x {nf} folds, 1 (alpha,c)) in {dt:.1f} s on 1 host core"}
+    return {"value": units * par / tn, "unit": "cells*folds*(alpha,c)/s", "cores": par, "kind": "port",
+            "host_cpus_online": os.cpu_count(),
+            "single_core_value": units / t1,
+            "sample": f"oracle/kp_oracle.c kpo_cv (1 thread per task) on sub-lattice {sub} of the same counts "
+                      f"({O.npat(sub)} cells x {nf} folds per (alpha,c) task): {par} concurrent tasks on "
+                      f"{par} host cores in {tn:.1f} s; 1 task alone on 1 core in {t1:.1f} s"}
 
 
 def committed_traffic(gen_pat, n_lanes, kernel_tag):
@@ -140,15 +193,47 @@ def committed_traffic(gen_pat, n_lanes, kernel_tag):
     return best
 
 
-def full_cv(plan, prep, rank, world):
-    """The whole 5x5 grid x 5 folds as the CV driver runs it: this rank's share of the
-    (alpha, fold) groups, one pass each, root read-out included."""
+def full_cv(prep, gen_pat, max_block, rank, world, model_world=8):
+    """The whole grid x folds as the CV driver runs it, timed from the fold split on:
+    fold split (host C++, overlapped with the plan's table upload on the GPU), count
+    tables, this rank's lane-granular share of the passes, root read-out.  At world 1 it
+    also runs the shares the ``model_world`` ranks of an 8-GPU job would get, one after
+    the other, and models that job's wall-clock as the serial setup plus the slowest
+    share (there is no data-path collective)."""
+    import threading
+    from kmerpapa_amd.CV_tools import fold_tables as _ft
     from kmerpapa_amd.engine import pack_passes
     from kmerpapa_amd.shard import rank_groups
+    engine.release_all()
     t0 = time.perf_counter()
-    mine = rank_groups(prep["groups"], rank, world)  # lane-granular share (15-16 lanes at N=8)
-    roots = [plan.run(p) for p in pack_passes(mine, min(plan.lanes_that_fit(), 8))]
-    return time.perf_counter() - t0, len(mine), roots
+    box = {}
+
+    def split():
+        box["f"] = _ft(prep["ctx"], prep["nfolds"], np.random.RandomState(1), prep["itype"])
+    th = threading.Thread(target=split)
+    th.start()  # the C++ fold split drops the GIL; the plan's tables upload meanwhile
+    plan = engine.get_plan(engine.get_device(prep["device"]), gen_pat, max_block)
+    th.join()
+    contexts, Mf, Uf = box["f"]
+    Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, plan.info["n_kmers"], prep["itype"])
+    plan.set_counts(Mk, Uk)
+    t_setup = time.perf_counter() - t0
+    cap = plan.lanes_that_fit()
+
+    def share(r, w):
+        ts = time.perf_counter()
+        mine = rank_groups(prep["groups"], r, w)
+        for p in pack_passes(mine, cap):
+            plan.run(p)
+        return time.perf_counter() - ts, sum(len(g[3]) for g in mine)
+    t_mine, lanes_mine = share(rank, world)
+    out = {"wall_s": t_setup + t_mine, "setup_s": t_setup, "passes_s": t_mine, "lanes": lanes_mine}
+    if world == 1 and model_world > 1:
+        shares = [share(r, model_world) for r in range(model_world)]
+        out["model"] = {"world": model_world, "share_s": [round(x[0], 4) for x in shares],
+                        "share_lanes": [x[1] for x in shares],
+                        "wall_s": t_setup + max(x[0] for x in shares)}
+    return out
 
 
 def main():
@@ -161,7 +246,7 @@ def main():
     ap.add_argument("--pattern", default=None, help="override the config's general pattern")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--max-block", type=int, default=0)
-    ap.add_argument("--no-full-cv", action="store_true", help="skip the full 5x5x5 CV wall-clock leg")
+    ap.add_argument("--no-full-cv", action="store_true", help="skip the full grid CV wall-clock leg")
     a = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -178,9 +263,10 @@ def main():
     gen_pat = cfg["gen_pat"]
     prep = prepare(gen_pat, alphas=cfg["alphas"], penalties=cfg["penalties"], nfolds=cfg["nfolds"])
     ndev = engine.device_count()
-    dev = engine.get_device(local % max(1, ndev))  # one GPU per rank (several ranks per GPU only in rehearsals)
+    prep["device"] = local % max(1, ndev)  # one GPU per rank (several ranks per GPU only in rehearsals)
+    dev = engine.get_device(prep["device"])
     t0 = time.time()
-    plan = engine.Plan(dev, gen_pat, a.max_block)
+    plan = engine.get_plan(dev.device, gen_pat, a.max_block)
     plan.set_counts(prep["Mk"], prep["Uk"])
     t_setup = time.time() - t0
     groups = prep["groups"]
@@ -197,49 +283,72 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
     barrier()
     t_start = time.perf_counter()
     stats = [step(a.warmup + s) for s in range(a.steps)]
     t_end = time.perf_counter()
     barrier()
-    elapsed = t_end - t_start
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(t_end - t_start)
 
     units_rank = sum(s["units"] for s in stats)
     units = units_rank * world
     dp_ms = sum(s["dp_ms"] for s in stats)
-    alg = sum(s["alg_bytes"] for s in stats)
-    achieved = alg / (dp_ms / 1e3) / 1e9
+    launches = sum(s["dp_launches"] for s in stats)
+    dp_s = dp_ms / 1e3
+    must = sum(s["gather_bytes"] for s in stats)  # (8 P_high + 4) B per unit, blocked sweep
+    naive = sum(s["alg_bytes"] for s in stats)     # SURVEY.md 8(d) per-cell figure
+    floor = 8.0 * units_rank                       # every row read once + written once
     lanes = len(groups[0][3])
     tag = engine.kernel_tag()
     tr = committed_traffic(gen_pat, lanes, tag)
 
-    # 9-mer 5-fold CV wall-clock (BASELINE.json's second metric): fold split (host, every
-    # rank) + this rank's passes, max over ranks
-    cv_wall = None
+    # BASELINE.json's second metric: the full grid CV wall-clock (fold split, setup, passes,
+    # root read-out), max over ranks; at N=1 also the modelled 8-GPU wall-clock
+    cv = None
     if not a.no_full_cv:
         barrier()
-        t_cv, n_mine, _ = full_cv(plan, prep, rank, world)
-        cv_wall = prep["t_fold_s"] + t_setup + t_cv
-        if dist is not None:
-            import torch
-            t = torch.tensor([cv_wall], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            cv_wall = float(t.item())
+        cv = full_cv(prep, gen_pat, a.max_block, rank, world)
+        cv["wall_s"] = max_over_ranks(cv["wall_s"])
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
-        passes_full_cv = math.ceil(len(groups) / world)
+        roof = {"bound": "hbm", "achieved": must / dp_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": must / dp_s / 1e9 / PEAK_HBM_GBS,
+                "traffic": (tr["hbm_bytes_per_pass"] if tr else None),
+                "kernel": "kp_dp_kernel (all launches of one pass)",
+                "kernel_ms_per_pass": dp_ms / a.steps, "launches_per_pass": launches / a.steps,
+                "avg_launch_ms": dp_ms / max(1, launches),
+                "bytes_per_unit": must / units_rank,
+                "basis": "achieved = bytes the blocked sweep must move per pass ((8 P_high + 4) B per unit: "
+                         "two child-row reads per high-position split pair + one score write; DESIGN.md 3) / "
+                         "HIP-event time of the pass's kp_dp_kernel launches",
+                "floor_bytes_per_unit": 8.0, "floor_frac": floor / dp_s / 1e9 / PEAK_HBM_GBS,
+                "naive_equivalent_bytes_per_unit": naive / units_rank,
+                "naive_equivalent_gbs": naive / dp_s / 1e9}
+        if tr:
+            roof["traffic_basis"] = ("L2-miss fabric traffic per pass: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE over "
+                                     "the pass's kp_dp_kernel dispatches; includes Infinity-Cache hits (an upper "
+                                     "bound on HBM bytes)")
+            roof["traffic_source"] = tr.get("source")
+            roof["traffic_gbs"] = tr["hbm_bytes_per_pass"] / (dp_s / a.steps) / 1e9
+            roof["traffic_frac"] = roof["traffic_gbs"] / PEAK_HBM_GBS
+        n_gpus = min(world, max(1, ndev))
         line = {
             "metric": "patterns scored/sec (lattice cells x folds x (alpha,c)), 9-mer 5-fold CV 5x5 grid"
                       if (a.config == "9mer" and not a.pattern) else
-                      f"patterns scored/sec, {a.config} config, general pattern {gen_pat}",
+                      f"patterns scored/sec, general pattern {gen_pat} ({a.config} config)",
             "value": units / elapsed,
             "unit": "cell-scores/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
+            "ranks": world,
+            "rehearsal": world > n_gpus,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": ms_step,
@@ -255,28 +364,17 @@ def main():
                        "name": a.config, "gen_pat": gen_pat, "cells": plan.info["npat"], "lanes_per_step": lanes,
                        "units_per_step": plan.info["npat"] * lanes, "block_cells": plan.info["block"],
                        "alphas": prep["alphas"], "penalties": prep["penalties"], "nfolds": prep["nfolds"]},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS,
-                         "traffic": (tr["hbm_bytes_per_pass"] if tr else None),
-                         "kernel": "kp_dp_kernel (all launches of one pass)",
-                         "alg_bytes_per_pass": alg / a.steps,
-                         "alg_bytes_per_unit": alg / units_rank,
-                         "basis": "SURVEY.md 8(d) per-unit algorithmic bytes x units / HIP-event time of the "
-                                  "pass's kp_dp_kernel launches; traffic = PMC HBM bytes per pass"},
-            "dp_kernel_ms_per_step": dp_ms / a.steps,
-            "dp_kernel_launches_per_step": sum(s["dp_launches"] for s in stats) / a.steps,
-            "dp_kernel_avg_launch_ms": dp_ms / max(1, sum(s["dp_launches"] for s in stats)),
+            "roofline": roof,
             "backtrack_ms_per_step": sum(s["backtrack_ms"] for s in stats) / a.steps,
-            "cv_full_grid_wall_s": cv_wall,
-            "cv_full_grid_wall_s_estimate": prep["t_fold_s"] + t_setup + passes_full_cv * ms_step / 1e3,
+            "cv_full_grid_wall_s": cv["wall_s"] if cv else None,
+            "cv_full_grid": cv,
             "fold_split_s": prep["t_fold_s"],
             "setup_s": t_setup,
             "kernel_tag": tag,
         }
-        if tr:
-            line["roofline"]["traffic_source"] = tr.get("source")
-            line["roofline"]["traffic_gbs"] = tr["hbm_bytes_per_pass"] / (dp_ms / a.steps / 1e3) / 1e9
-            line["roofline"]["traffic_frac"] = line["roofline"]["traffic_gbs"] / PEAK_HBM_GBS
+        if cv and "model" in cv:
+            line["cv_full_grid_wall_s_model_8gpu"] = cv["model"]["wall_s"]
+            line["cv_full_grid_speedup_model_8gpu"] = cv["wall_s"] / cv["model"]["wall_s"]
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(prep)
         else:

@@ -67,7 +67,8 @@ typedef struct {
     int32_t k, low_positions, max_level, high_levels;
     double pairs_total;   /* split pairs summed over all cells (SURVEY 8d "P")    */
     double pairs_high;    /* ... of which at high (gathered) positions             */
-    uint64_t bytes_per_lane; /* device bytes per lane (train f32 + argmin u8)     */
+    uint64_t bytes_per_lane; /* device bytes per lane: f32 train score per cell
+                                (value-only sweep) + backtrack node pool + leaves */
 } kp_plan_info;
 
 typedef struct {

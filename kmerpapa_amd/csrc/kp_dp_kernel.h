@@ -44,7 +44,7 @@ struct kp_dp_params {
     int lanesplit;  // split a cell's lanes over threads on narrow levels (KP_LANE_SPLIT=0 disables)
     int ntstore;    // 1 = score rows stored non-temporally (default; KP_NT_STORE=0 for plain stores)
     unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
-    int dbg;  // timing ablation only (KP_DEBUG_SKIP, wrong results): 1 = skip gather, 2 = skip level phase,
+    int dbg;  // -DKP_ABLATION builds only (KP_DEBUG_SKIP, wrong results; always 0 otherwise): 1 = skip gather, 2 = skip level phase,
               // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier
 };
 
@@ -62,6 +62,13 @@ struct kp_dp_params {
 #define KP_STAMP(slot) \
     do {               \
     } while (0)
+#endif
+
+// phase skipping of the timing-ablation build (-DKP_ABLATION); constant false otherwise
+#ifdef KP_ABLATION
+#define KP_SKIP(P, bit) (((P).dbg & (bit)) != 0)
+#else
+#define KP_SKIP(P, bit) false
 #endif
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
@@ -193,7 +200,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     // one pair per lane
     const uint64_t hd = P.T.hdig[P.hbase + widx];
     int np = 0;
-    if (!(P.dbg & 1))
+    if (!KP_SKIP(P, 1))
         for (int i = 0; i < g.kh; ++i) np += P.T.tabs[g.t + i].np[(hd >> (4 * i)) & 15u];
     const uint64_t rowstride = (uint64_t)g.Ltot * Bpad;
     for (int p = (int)threadIdx.x; threadIdx.x < 64 && p < np; p += 64) {  // wave 0
@@ -231,7 +238,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
     // the next level's descriptors are loaded while the current level computes
     const bool high_zero = (P.H == 0);
-    const int lmax = (P.dbg & 2) ? -1 : P.lmax;
+    const int lmax = KP_SKIP(P, 2) ? -1 : P.lmax;
     const uint4 *desc = reinterpret_cast<const uint4 *>(P.T.ldesc);
     // narrow levels (cells x lanes <= threads, e.g. the block's top levels) split each
     // cell's lanes over NL threads: the same work with a 1/NL-long dependent chain
@@ -267,7 +274,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         if (lane_split(cnt)) {
             const int q = (int)threadIdx.x / NL;
             const uint32_t j = threadIdx.x % NL;
-            if (q < cnt && !(P.dbg & 8)) {
+            if (q < cnt && !KP_SKIP(P, 8)) {
                 const uint32_t l = cur[0].x & 0xFFFFu;
                 const uint32_t info = cur[0].z;
                 const uint32_t npairs = cur[0].w & 0xFFu;
@@ -310,12 +317,12 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                 sc.kmer = high_zero && lam == 0;
                 sc.c.mte = sc.c.ute = 0;
                 sc.logp = sc.log1mp = 0.0;
-                if (!sc.kmer && !(P.dbg & 4)) {
+                if (!sc.kmer && !KP_SKIP(P, 4)) {
                     const double pr = kp_rate(sc.c, alpha, beta);
                     sc.logp = log(pr);
                     sc.log1mp = log(1.0 - pr);
                 }
-                if (!(P.dbg & 8)) {
+                if (!KP_SKIP(P, 8)) {
                     kp_dp_cell_list<NL, NL>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, pen);
                 } else {  // timing ablation: no split scan, keep the single term
 #pragma unroll
@@ -324,7 +331,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                 }
             }
         }
-        if (!(P.dbg & 16)) __syncthreads();  // (ablation 16: timing without the level barrier)
+        if (!KP_SKIP(P, 16)) __syncthreads();  // (ablation 16: timing without the level barrier)
         KP_STAMP(3 + lam);
 #pragma unroll
         for (int k = 0; k < KP_IPT; ++k) cur[k] = nxt[k];

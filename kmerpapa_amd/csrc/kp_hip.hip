@@ -735,7 +735,13 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.lmax = hp.lmax;
     P.ptab_entries = hp.ptab_entries;
     P.pscratch_entries = hp.pscratch_entries;
+#ifdef KP_ABLATION
+    // timing-ablation build only (make ablation -> libkmerpapa_hip_ablation.so): phases
+    // skipped by KP_DEBUG_SKIP give wrong scores, so the pass reports KP_E_STATE below
     P.dbg = getenv("KP_DEBUG_SKIP") ? atoi(getenv("KP_DEBUG_SKIP")) : 0;
+#else
+    P.dbg = 0;  // the product build has no phase-skipping path
+#endif
     // runs of 8 consecutive blocks per XCD (workgroups are dealt round-robin over the 8
     // XCDs): neighbours in the reuse order share their L2; measured -1 %
     P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 8;
@@ -828,6 +834,13 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     }
 #endif
     KP_HIP(hipEventElapsedTime(&bt_ms, c->ev[1], c->ev[2]));
+    if (P.dbg) {  // ablation build: timings only, never numbers
+        p->stats.dp_ms = dp_ms;
+        p->stats.backtrack_ms = 0;
+        p->stats.units = hp.npat * (uint64_t)Ltot;
+        p->stats.dp_launches = launches;
+        return fail(KP_E_STATE, "KP_DEBUG_SKIP ablation pass: timings only, results are invalid");
+    }
     for (uint32_t i = 0; i < Ltot; ++i) {
         if (bad[i])
             return fail(KP_E_PARITY, "backtrack of lane " + std::to_string(i) + " failed (flags " +

@@ -8,7 +8,8 @@ Host-side responsibilities kept here:
   * k-mer ordering: count tables go to the device in KmerEnumeration order (position 0
     fastest, nucleotide digit = index in ``code[g]``), see ``kmer_order``;
   * pass planning: lane groups are packed into passes that fit device memory
-    (5 bytes per cell per lane: f32 train score + u8 argmin code);
+    (4 bytes per cell per lane: the f32 train score of the value-only sweep, plus a
+    per-lane backtrack node pool; ``Plan.info["bytes_per_lane"]``);
   * sharding: groups are spread over the visible GPUs, one host thread per GPU
     (ctypes releases the GIL during every call), no collective needed.
 """
@@ -113,15 +114,25 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+# launch knobs read by kp_hip.hip (every setting gives the same scores; they change timing)
+LAUNCH_KNOBS = ("KP_DP_THREADS", "KP_LANES_PER_WG", "KP_XCD_REMAP", "KP_LANE_SPLIT", "KP_NT_STORE")
+
+
 def kernel_tag():
-    """Short hash of the sweep kernel's sources (kp_core.h, kp_dp_kernel.h, kp_plan.h):
-    ties PMC profiles to the kernel build they measured."""
+    """Short hash of everything that decides the sweep's launches: every source of the
+    library (csrc/*, the C-ABI header) and the launch knobs set in the environment.  Ties
+    PMC profiles (profiles/*/pmc_*.json) to the exact build and launch configuration."""
+    import glob
     import hashlib
     h = hashlib.sha1()
-    src = os.path.join(_HERE, "csrc")
-    for name in ("kp_core.h", "kp_dp_kernel.h", "kp_plan.h"):
-        with open(os.path.join(src, name), "rb") as f:
-            h.update(name.encode() + b"\0" + f.read())
+    files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*")))
+    files.append(os.path.join(os.path.dirname(_HERE), "include", "kmerpapa_hip.h"))
+    for fn in files:
+        if os.path.isfile(fn) and not fn.endswith((".s", ".o")):
+            with open(fn, "rb") as f:
+                h.update(os.path.basename(fn).encode() + b"\0" + f.read())
+    for k in LAUNCH_KNOBS:
+        h.update(f"{k}={os.environ.get(k, '')}".encode())
     return h.hexdigest()[:12]
 
 
@@ -400,26 +411,30 @@ def release_all():
 def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     """Run every lane group over the lattice of ``gen_pat`` on the given GPUs.
 
-    ``M``/``U`` are ``[n_kmers, nf]`` counts in k-mer order.  Groups are dealt out in
-    contiguous chunks (one chunk per GPU), each chunk packed into memory-sized passes.
-    Returns ``(root_train, root_test, n_leaves)`` arrays over all lanes, group-major.
+    ``M``/``U`` are ``[n_kmers, nf]`` counts in k-mer order.  The lanes (one penalty of one
+    group, group-major) are cut into one contiguous, equal run per GPU and regrouped by
+    (fold, alpha) (``shard.rank_groups``, the same lane-granular split the ranks of a
+    torchrun job use), each GPU's share packed into memory-sized passes, one host thread
+    per GPU.  Returns ``(root_train, root_test, n_leaves)`` arrays over all lanes,
+    group-major.
     """
     devices = list(devices) if devices is not None else visible_devices()[:1]
     devices = list(dict.fromkeys(devices))  # one host thread per GPU: a device's plan is not shared
     if not devices:
         raise KPError(-3, "no GPU visible")
-    from .shard import chunk_bounds
-    bounds = chunk_bounds([len(g[3]) for g in groups], len(devices))  # contiguous, lane-balanced
-    results = [None] * len(devices)
+    from .shard import rank_groups
+    nd = len(devices)
+    results = [None] * nd
     errors = []
 
     def work(slot, dev, chunk):
         try:
-            plan = get_plan(dev, gen_pat, max_block)
-            plan.set_counts(M, U)
             outs = []
-            for pas in pack_passes(chunk, plan.lanes_that_fit()):
-                outs.append(plan.run(pas))
+            if chunk:
+                plan = get_plan(dev, gen_pat, max_block)
+                plan.set_counts(M, U)
+                for pas in pack_passes(chunk, plan.lanes_that_fit()):
+                    outs.append(plan.run(pas))
             if outs:
                 results[slot] = tuple(np.concatenate([o[i] for o in outs]) for i in range(3))
             else:
@@ -429,8 +444,8 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
 
     threads = []
     for slot, dev in enumerate(devices):
-        chunk = groups[bounds[slot]:bounds[slot + 1]]
-        if len(devices) == 1:
+        chunk = rank_groups(groups, slot, nd)  # slots in order = lanes in order
+        if nd == 1:
             work(slot, dev, chunk)
         else:
             th = threading.Thread(target=work, args=(slot, dev, chunk))

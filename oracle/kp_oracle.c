@@ -25,8 +25,12 @@
  *  - level 0 uses xlogy / xlog1py (scipy: 0 if x == 0 and y is not NaN) in the order
  *    -2*(a+b)+c; levels >= 1 use log(p), log(1-p) in the order c + a + b.
  *  Build with -ffp-contract=off (no fused multiply-add), -O2, no fast-math.
+ *  - nthreads > 1 splits each level's cells over OpenMP threads: a cell reads only cells of
+ *    strictly lower levels, so every value is the same as with one thread (the reference
+ *    walks a level in any order it likes, CV :156, Fit :119).
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -128,7 +132,7 @@ uint64_t kpo_npat(const char *gp) {
  *   score, test : [npat][nf] float32 outputs (train score and test -2LL of every cell).
  */
 int kpo_cv(const char *gp, int nf, uint64_t *M, uint64_t *U, int itype_bits,
-           double alpha, const double *betas, double penalty, float *score, float *test) {
+           double alpha, const double *betas, double penalty, float *score, float *test, int nthreads) {
     kpo_lat L;
     if (lat_build(gp, &L) || nf <= 0 || nf > 64) return -1;
     const uint64_t mask = itype_bits >= 64 ? ~0ULL : ((1ULL << itype_bits) - 1);
@@ -136,9 +140,12 @@ int kpo_cv(const char *gp, int nf, uint64_t *M, uint64_t *U, int itype_bits,
     uint64_t *ord = level_order(&L, off);
     if (!ord) return -2;
     const float inf32 = (float)1e100; /* np.full(..., 1e100, float32) -> +inf (CV :143) */
+    const int nt = nthreads > 0 ? nthreads : 1;
+#pragma omp parallel for num_threads(nt) schedule(static)
     for (uint64_t n = 0; n < L.npat * (uint64_t)nf; ++n) { score[n] = inf32; test[n] = 0.0f; }
 
     /* level 0: score_test_folds (CV :15-20) on every k-mer row, get_train (:22-24) */
+#pragma omp parallel for num_threads(nt) schedule(static)
     for (uint64_t q = off[0]; q < off[1]; ++q) {
         uint64_t n = ord[q];
         const uint64_t *m = M + n * nf, *u = U + n * nf;
@@ -153,8 +160,10 @@ int kpo_cv(const char *gp, int nf, uint64_t *M, uint64_t *U, int itype_bits,
             test[n * nf + f] = (float)te;
         }
     }
-    /* levels >= 1: handle_pattern (CV :26-78) */
-    for (uint64_t q = off[1]; q < off[L.maxlev + 1]; ++q) {
+    /* levels >= 1: handle_pattern (CV :26-78), one level after the other */
+    for (int lev = 1; lev <= L.maxlev; ++lev)
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (uint64_t q = off[lev]; q < off[lev + 1]; ++q) {
         uint64_t n = ord[q];
         float *rs = score + n * nf, *rt = test + n * nf;
         int first = 1;
@@ -210,7 +219,7 @@ int kpo_cv(const char *gp, int nf, uint64_t *M, uint64_t *U, int itype_bits,
  *               or the cell itself when it is kept whole), as Fit :46-49, :62-64.
  */
 int kpo_fit(const char *gp, uint64_t *M, uint64_t *U, int itype_bits, double alpha, double beta,
-            double penalty, float *score, uint64_t *backtrack) {
+            double penalty, float *score, uint64_t *backtrack, int nthreads) {
     kpo_lat L;
     if (lat_build(gp, &L)) return -1;
     const uint64_t mask = itype_bits >= 64 ? ~0ULL : ((1ULL << itype_bits) - 1);
@@ -218,8 +227,11 @@ int kpo_fit(const char *gp, uint64_t *M, uint64_t *U, int itype_bits, double alp
     uint64_t *ord = level_order(&L, off);
     if (!ord) return -2;
     const float inf32 = (float)1e100;
+    const int nt = nthreads > 0 ? nthreads : 1;
+#pragma omp parallel for num_threads(nt) schedule(static)
     for (uint64_t n = 0; n < L.npat; ++n) score[n] = inf32;
     /* level 0: score(M, U) (Fit :26-29, :106-114) */
+#pragma omp parallel for num_threads(nt) schedule(static)
     for (uint64_t q = off[0]; q < off[1]; ++q) {
         uint64_t n = ord[q];
         double m = (double)M[n], u = (double)U[n];
@@ -227,8 +239,10 @@ int kpo_fit(const char *gp, uint64_t *M, uint64_t *U, int itype_bits, double alp
         score[n] = (float)(-2.0 * (xlogy_(m, p) + xlog1py_(u, -p)) + penalty);
         backtrack[n] = n;
     }
-    /* levels >= 1: handle_pattern (Fit :31-64) */
-    for (uint64_t q = off[1]; q < off[L.maxlev + 1]; ++q) {
+    /* levels >= 1: handle_pattern (Fit :31-64), one level after the other */
+    for (int lev = 1; lev <= L.maxlev; ++lev)
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (uint64_t q = off[lev]; q < off[lev + 1]; ++q) {
         uint64_t n = ord[q];
         int first = 1;
         uint64_t rest = n;

@@ -45,10 +45,10 @@ def lib():
         L.kpo_npat.argtypes = [ctypes.c_char_p]
         L.kpo_npat.restype = ctypes.c_uint64
         L.kpo_cv.argtypes = [ctypes.c_char_p, ctypes.c_int, u64p, u64p, ctypes.c_int, ctypes.c_double,
-                             f64p, ctypes.c_double, f32p, f32p]
+                             f64p, ctypes.c_double, f32p, f32p, ctypes.c_int]
         L.kpo_cv.restype = ctypes.c_int
         L.kpo_fit.argtypes = [ctypes.c_char_p, u64p, u64p, ctypes.c_int, ctypes.c_double, ctypes.c_double,
-                              ctypes.c_double, f32p, u64p]
+                              ctypes.c_double, f32p, u64p, ctypes.c_int]
         L.kpo_fit.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -86,8 +86,9 @@ def _scatter(gen_pat, contexts, rows, nf):
     return arr
 
 
-def cv_pass(gen_pat, contexts, Mf, Uf, alpha, betas, penalty, itype_bits=32):
+def cv_pass(gen_pat, contexts, Mf, Uf, alpha, betas, penalty, itype_bits=32, threads=1):
     """One CV pass for a single (alpha, penalty) over all folds (CV module :143-163).
+    ``threads`` > 1 splits every level over OpenMP threads (same values).
 
     ``contexts`` are k-mers and ``Mf``/``Uf`` their ``[n_kmers, nf]`` fold counts.
     Returns a dict with the full ``score``/``test``/``M``/``U`` arrays and the root rows.
@@ -102,7 +103,7 @@ def cv_pass(gen_pat, contexts, Mf, Uf, alpha, betas, penalty, itype_bits=32):
     b = np.ascontiguousarray(betas, dtype=np.float64)
     rc = lib().kpo_cv(gen_pat.encode(), nf, _ptr(M, ctypes.c_uint64), _ptr(U, ctypes.c_uint64),
                       int(itype_bits), float(alpha), _ptr(b, ctypes.c_double), float(penalty),
-                      _ptr(score, ctypes.c_float), _ptr(test, ctypes.c_float))
+                      _ptr(score, ctypes.c_float), _ptr(test, ctypes.c_float), int(threads))
     if rc:
         raise RuntimeError(f"kpo_cv failed ({rc})")
     root = cell_index(gen_pat, gen_pat)
@@ -141,7 +142,7 @@ def names_from_backtrack(gen_pat, bt):
     return out
 
 
-def fit(gen_pat, contexts, M0, U0, alpha, beta, penalty, itype_bits=32):
+def fit(gen_pat, contexts, M0, U0, alpha, beta, penalty, itype_bits=32, threads=1):
     """Fit DP + backtrack (Fit :67-124).  Returns (score_f32, M_root, U_root, names, arrays)."""
     M = _scatter(gen_pat, contexts, np.asarray(M0).reshape(-1, 1), 1).reshape(-1)
     U = _scatter(gen_pat, contexts, np.asarray(U0).reshape(-1, 1), 1).reshape(-1)
@@ -150,7 +151,7 @@ def fit(gen_pat, contexts, M0, U0, alpha, beta, penalty, itype_bits=32):
     bt = np.empty(n, dtype=np.uint64)
     rc = lib().kpo_fit(gen_pat.encode(), _ptr(M, ctypes.c_uint64), _ptr(U, ctypes.c_uint64),
                        int(itype_bits), float(alpha), float(beta), float(penalty),
-                       _ptr(score, ctypes.c_float), _ptr(bt, ctypes.c_uint64))
+                       _ptr(score, ctypes.c_float), _ptr(bt, ctypes.c_uint64), int(threads))
     if rc:
         raise RuntimeError(f"kpo_fit failed ({rc})")
     root = cell_index(gen_pat, gen_pat)

@@ -12,6 +12,7 @@ Canonical interpreter: /opt/conda/bin/python3.9 (numpy 1.26, scipy 1.7) which fo
 the numpy<2 promotion rules of the reference's pinned numpy 1.23.3.
 
 Usage:  python3 tests/golden/make_golden.py [--jobs small,grid5,fit5,cli5,cli5b,fit7,cv7,allk5]
+        (config 3 grid: one process per point, --jobs cv7p_<alpha>_<c>, then --jobs cv7merge)
 The GPU box never runs this file (no /root/reference there).
 """
 import argparse
@@ -449,6 +450,43 @@ def job_cv7(out):
                    "best": [res[0], res[1], float(res[2])], "cvfile": cvtext, "passes": recs}, fh)
 
 
+CV7_ALPHAS = [0.5, 1.0, 10.0]
+CV7_PENALTIES = [3.0, 5.0, 7.0]
+
+
+def job_cv7p(out, alpha, penalty):
+    """One grid point of the 7-mer 3x3 grid (config 3), run the way the reference's README
+    fans a grid out (README.md:39-51: one --CV_only process per (c, a), same seed, so the
+    same fold split): roots of every fold and the CVfile row of that point."""
+    ctx, gp, nu, nm = _context(7)
+    res, log, cvtext = _run_cv(ctx, gp, [alpha], [penalty], 5, 1, nm, nu, False)
+    recs = [{"alpha": r["alpha"], "penalty": r["penalty"], "betas": r["betas"],
+             "root_train": [float(x) for x in r["root_train"]],
+             "root_test": [float(x) for x in r["root_test"]]} for r in log]
+    os.makedirs(os.path.join(out, "cv7_points"), exist_ok=True)
+    with open(os.path.join(out, "cv7_points", f"a{alpha}_c{penalty}.json"), "w") as fh:
+        json.dump({"gen_pat": gp, "alpha": alpha, "penalty": penalty, "nfolds": 5, "seed": 1,
+                   "best": [res[0], res[1], float(res[2])], "cvfile": cvtext, "passes": recs}, fh)
+
+
+def job_cv7merge(out):
+    """Merge the nine cv7 points into cv7.json: CVfile rows in the reference's alpha-major,
+    c-minor order (CV :165-177) and the grid's best point (strict "<" in that order)."""
+    pts = []
+    for a in CV7_ALPHAS:
+        for c in CV7_PENALTIES:
+            with open(os.path.join(out, "cv7_points", f"a{a}_c{c}.json")) as fh:
+                pts.append(json.load(fh))
+    best = None
+    for p in pts:
+        if best is None or p["best"][2] < best[2]:
+            best = p["best"]
+    with open(os.path.join(out, "cv7.json"), "w") as fh:
+        json.dump({"gen_pat": pts[0]["gen_pat"], "alphas": CV7_ALPHAS, "penalties": CV7_PENALTIES,
+                   "nfolds": 5, "seed": 1, "best": best, "cvfile": "".join(p["cvfile"] for p in pts),
+                   "passes": [p["passes"][0] for p in pts]}, fh)
+
+
 def job_data(out):
     """The reference's k-mer count files as one npz (inputs of configs 1-3)."""
     import numpy as np
@@ -463,6 +501,10 @@ def job_data(out):
 
 
 def _child(job, out):
+    if job.startswith("cv7p_"):  # cv7p_<alpha>_<penalty>
+        _, a, c = job.split("_")
+        job_cv7p(out, float(a), float(c))
+        return
     globals()["job_" + job](out)
 
 
@@ -476,8 +518,8 @@ def main():
     if a.child:
         _child(a.child, a.out)
         return
-    if a.jobs == "data":
-        job_data(a.out)
+    if a.jobs in ("data", "cv7merge"):
+        globals()["job_" + a.jobs](a.out)
         return
     with tempfile.TemporaryDirectory() as tmp:
         make_shim(tmp)

@@ -200,22 +200,6 @@ def test_fit7_partition(eng):
     assert names == fo["names"]
 
 
-def test_cv7_roots_vs_oracle(eng):
-    """7-mer test data (34,171,875 cells), 5-fold CV through the drop-in driver: every
-    fold's root train/test value equals the oracle's (pinned to the reference), bit for
-    bit.  (The reference itself needs hours per pass here, so the oracle is the checker.)"""
-    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
-    from kmerpapa_amd.CV_tools import fold_tables
-    from oracle import oracle as O
-    ctx, gp, nm, nu = context_table(7)
-    alphas, pens = [1.0], [5.0, 3.0]
-    res = cvm.cv_roots(gp, ctx, alphas, pens, 5, 1, 1, np.uint32, devices=[0])
-    contexts, Mf, Uf = fold_tables(ctx, 5, np.random.RandomState(1), np.uint32)
-    ref = O.cv_pass(gp, contexts, Mf, Uf, alphas[0], res["betas"][0, 0], pens[0], 32)
-    assert bits_equal(res["train"][0, 0, 0], ref["root_train"])
-    assert bits_equal(res["test"][0, 0, 0], ref["root_test"])
-
-
 def test_9mer_sublattice_fit_vs_oracle(eng):
     """Synthetic 9-mer counts of the benchmark restricted to ANNNMNNNA (34M cells): the fit
     (score, M, U, partition in backtrack order) equals the oracle's."""

@@ -94,3 +94,41 @@ def test_two_rank_gloo_cv_matches_single_process():
     want = [(f, a, p) for a in c["alphas"] for f in range(c["nfolds"]) for p in c["penalties"]]
     assert sorted(ran_all) == sorted(want)  # every lane (alpha, fold, penalty) exactly once over both ranks
     assert all(len(r) > 0 for _, _, _, r in outs)  # both ranks did work
+
+
+def test_engine_run_groups_lane_granular_over_devices(monkeypatch):
+    """engine.run_groups splits the lanes over the GPUs of one process like the ranks of a
+    torchrun job (contiguous equal runs, regrouped by (fold, alpha)) and returns them in
+    the original lane order; every lane runs exactly once.  A stand-in plan replaces the
+    GPU (each lane's "root" encodes its (fold, alpha, penalty))."""
+    from kmerpapa_amd import engine
+    ran = {}
+
+    class FakePlan:
+        def __init__(self, dev):
+            self.dev = dev
+
+        def set_counts(self, M, U):
+            pass
+
+        def lanes_that_fit(self):
+            return 7
+
+        def run(self, groups):
+            lanes = [(g[0], g[1], c) for g in groups for c in g[3]]
+            for ln in lanes:
+                ran.setdefault(ln, []).append(self.dev)
+            rt = np.array([f * 1000 + a * 10 + c for f, a, c in lanes], np.float32)
+            return rt, -rt, np.arange(len(lanes), dtype=np.uint64)
+    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0: FakePlan(dev))
+    groups = [(f, a, 0.1, [3.0, 4.0, 5.0, 6.0, 7.0]) for a in (0.5, 1.0, 2.0, 5.0, 10.0) for f in range(5)]
+    want = np.array([f * 1000 + a * 10 + c for f, a, _, pens in groups for c in pens], np.float32)
+    for devs in ([0], [0, 1], [0, 1, 2], [3, 2, 1, 0, 4, 5, 6, 7]):
+        ran.clear()
+        rt, re, _ = engine.run_groups("NMN", None, None, groups, devices=devs)
+        assert np.array_equal(rt, want) and np.array_equal(re, -want)
+        assert len(ran) == 125 and all(len(v) == 1 for v in ran.values())
+        per_dev = {}
+        for v in ran.values():
+            per_dev[v[0]] = per_dev.get(v[0], 0) + 1
+        assert sorted(per_dev) == sorted(devs) and max(per_dev.values()) - min(per_dev.values()) <= 1
