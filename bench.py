@@ -212,7 +212,7 @@ def full_cv(prep, gen_pat, max_block, rank, world, model_world=8):
         box["f"] = _ft(prep["ctx"], prep["nfolds"], np.random.RandomState(1), prep["itype"])
     th = threading.Thread(target=split)
     th.start()  # the C++ fold split drops the GIL; the plan's tables upload meanwhile
-    plan = engine.get_plan(engine.get_device(prep["device"]), gen_pat, max_block)
+    plan = engine.get_plan(prep["device"], gen_pat, max_block)
     th.join()
     contexts, Mf, Uf = box["f"]
     Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, plan.info["n_kmers"], prep["itype"])

@@ -12,6 +12,7 @@ from kmerpapa_amd import engine  # noqa: E402
 
 d, out = sys.argv[1], sys.argv[2]
 lanes = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+gen_pat = sys.argv[4] if len(sys.argv) > 4 else "NNNNMNNNN"
 
 
 def total(pass_name, counter):
@@ -26,10 +27,15 @@ def total(pass_name, counter):
 
 fetch, nf = total("fetch", "FETCH_SIZE")
 write, nw = total("write", "WRITE_SIZE")
-rec = {"gen_pat": "NNNNMNNNN", "lanes": lanes, "kernel_tag": engine.kernel_tag(),
+l2 = {c: total("l2", c)[0] for c in ("TCC_HIT_sum", "TCC_MISS_sum")}
+rec = {"gen_pat": gen_pat, "lanes": lanes, "kernel_tag": engine.kernel_tag(),
        "dp_launches": nf, "fetch_size_kb": fetch, "write_size_kb": write,
        "hbm_read_bytes_per_pass": 2 * fetch * 1024, "hbm_write_bytes_per_pass": write * 1024,
        "hbm_bytes_per_pass": 2 * fetch * 1024 + write * 1024,
+       "tcc_hit": l2["TCC_HIT_sum"], "tcc_miss": l2["TCC_MISS_sum"],
+       "tcc_hit_rate": (l2["TCC_HIT_sum"] / (l2["TCC_HIT_sum"] + l2["TCC_MISS_sum"])
+                        if l2["TCC_HIT_sum"] + l2["TCC_MISS_sum"] > 0 else None),
+       "basis": "L2-miss fabric traffic (FETCH_SIZE x2 + WRITE_SIZE): includes Infinity-Cache hits",
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of "
                  "`bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-full-cv`, kp_dp_kernel dispatches "
                  "summed; FETCH_SIZE x2 (gfx950 16-B/lane read correction), KB x1024"}
