@@ -193,46 +193,42 @@ def committed_traffic(gen_pat, n_lanes, kernel_tag):
     return best
 
 
-def full_cv(prep, gen_pat, max_block, rank, world, model_world=8):
-    """The whole grid x folds as the CV driver runs it, timed from the fold split on:
-    fold split (host C++, overlapped with the plan's table upload on the GPU), count
-    tables, this rank's lane-granular share of the passes, root read-out.  At world 1 it
-    also runs the shares the ``model_world`` ranks of an 8-GPU job would get, one after
-    the other, and models that job's wall-clock as the serial setup plus the slowest
-    share (there is no data-path collective)."""
-    import threading
-    from kmerpapa_amd.CV_tools import fold_tables as _ft
+def cv_shares(prep, world, cap):
+    """The passes each of ``world`` ranks runs for the full grid (lane-granular shares,
+    kmerpapa_amd.shard.rank_groups, packed into passes of at most ``cap`` lanes)."""
     from kmerpapa_amd.engine import pack_passes
     from kmerpapa_amd.shard import rank_groups
-    engine.release_all()
-    t0 = time.perf_counter()
-    box = {}
+    return [pack_passes(rank_groups(prep["groups"], r, world), cap) for r in range(world)]
 
-    def split():
-        box["f"] = _ft(prep["ctx"], prep["nfolds"], np.random.RandomState(1), prep["itype"])
-    th = threading.Thread(target=split)
-    th.start()  # the C++ fold split drops the GIL; the plan's tables upload meanwhile
-    plan = engine.get_plan(prep["device"], gen_pat, max_block)
-    th.join()
-    contexts, Mf, Uf = box["f"]
+
+def full_cv(plan, prep, gen_pat, rank, world, cap, model_world=8):
+    """The whole grid x folds as the CV driver runs it, on the already-built plan (its
+    table upload and lane allocation are timed at start-up, ``t_plan`` / ``t_reserve``):
+    fold split (host C++), count tables, this rank's lane-granular share of the passes,
+    root read-out.  At world 1 it also runs the shares the ``model_world`` ranks of an
+    8-GPU job would get, one after the other, and models that job's wall-clock as the
+    serial setup plus the slowest share (there is no data-path collective)."""
+    from kmerpapa_amd.CV_tools import fold_tables as _ft
+    t0 = time.perf_counter()
+    contexts, Mf, Uf = _ft(prep["ctx"], prep["nfolds"], np.random.RandomState(1), prep["itype"])
     Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, plan.info["n_kmers"], prep["itype"])
     plan.set_counts(Mk, Uk)
     t_setup = time.perf_counter() - t0
-    cap = plan.lanes_that_fit()
 
-    def share(r, w):
+    def share(passes):
         ts = time.perf_counter()
-        mine = rank_groups(prep["groups"], r, w)
-        for p in pack_passes(mine, cap):
+        for p in passes:
             plan.run(p)
-        return time.perf_counter() - ts, sum(len(g[3]) for g in mine)
-    t_mine, lanes_mine = share(rank, world)
-    out = {"wall_s": t_setup + t_mine, "setup_s": t_setup, "passes_s": t_mine, "lanes": lanes_mine}
+        return time.perf_counter() - ts, sum(len(g[3]) for p in passes for g in p)
+    t_mine, lanes_mine = share(cv_shares(prep, world, cap)[rank])
+    fixed = prep["t_plan"] + prep["t_reserve"]
+    out = {"wall_s": fixed + t_setup + t_mine, "plan_and_alloc_s": fixed, "fold_split_and_counts_s": t_setup,
+           "passes_s": t_mine, "lanes": lanes_mine}
     if world == 1 and model_world > 1:
-        shares = [share(r, model_world) for r in range(model_world)]
+        shares = [share(p) for p in cv_shares(prep, model_world, cap)]
         out["model"] = {"world": model_world, "share_s": [round(x[0], 4) for x in shares],
                         "share_lanes": [x[1] for x in shares],
-                        "wall_s": t_setup + max(x[0] for x in shares)}
+                        "wall_s": fixed + t_setup + max(x[0] for x in shares)}
     return out
 
 
@@ -265,11 +261,19 @@ def main():
     ndev = engine.device_count()
     prep["device"] = local % max(1, ndev)  # one GPU per rank (several ranks per GPU only in rehearsals)
     dev = engine.get_device(prep["device"])
-    t0 = time.time()
+    t0 = time.perf_counter()
     plan = engine.get_plan(dev.device, gen_pat, a.max_block)
+    prep["t_plan"] = time.perf_counter() - t0
     plan.set_counts(prep["Mk"], prep["Uk"])
-    t_setup = time.time() - t0
+    t_setup = time.perf_counter() - t0
     groups = prep["groups"]
+    # one allocation for the largest pass of the run (re-allocating large buffers is slow)
+    cap = min(plan.lanes_that_fit(), 8)
+    most = max([len(groups[0][3])] + [sum(len(g[3]) for g in p) for w in (world, 8) if not a.no_full_cv
+                                      for passes in cv_shares(prep, w, cap) for p in passes])
+    t0 = time.perf_counter()
+    plan.reserve(most)
+    prep["t_reserve"] = time.perf_counter() - t0
 
     def step(s):
         g = groups[(s * world + rank) % len(groups)]
@@ -315,7 +319,7 @@ def main():
     cv = None
     if not a.no_full_cv:
         barrier()
-        cv = full_cv(prep, gen_pat, a.max_block, rank, world)
+        cv = full_cv(plan, prep, gen_pat, rank, world, cap)
         cv["wall_s"] = max_over_ranks(cv["wall_s"])
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
@@ -370,6 +374,9 @@ def main():
             "cv_full_grid": cv,
             "fold_split_s": prep["t_fold_s"],
             "setup_s": t_setup,
+            "plan_s": prep["t_plan"],
+            "reserve_s": prep["t_reserve"],
+            "reserved_lanes": most,
             "kernel_tag": tag,
         }
         if cv and "model" in cv:

@@ -107,6 +107,14 @@ int kp_pass(kp_plan *plan, const kp_group *groups, int n_groups, float *root_tra
             uint64_t *n_leaves);
 int kp_last_pass_stats(const kp_plan *plan, kp_pass_stats *out);
 
+/* Allocate the per-lane device buffers (score rows, backtrack nodes) for `lanes` lanes now,
+ * so that later passes of up to that many lanes allocate nothing.  Buffers only grow.
+ * Re-allocating after a free is slow on MI355X (freed HBM is wiped first), so a job that
+ * knows its largest pass should reserve it once.  KP_E_NOMEM if it does not fit.
+ * (No reference counterpart: the reference allocates its [npat, nf] arrays per call, CV
+ * :93-102.) */
+int kp_reserve_lanes(kp_plan *plan, uint32_t lanes);
+
 /* Leaves (cell indices) of lane `lane` of the last pass, in the reference's backtrack
  * order.  cap = capacity of `leaves`; *n_out = number of leaves. */
 int kp_fit_leaves(kp_plan *plan, uint32_t lane, uint64_t *leaves, uint64_t cap, uint64_t *n_out);

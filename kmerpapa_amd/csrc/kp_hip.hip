@@ -640,6 +640,32 @@ static int lanes_per_wg_default() {
     return std::min(std::max(v, 1), KP_GROUP_LANES);
 }
 
+// Score rows + backtrack node pool for `lanes` lanes.  Grown only (a pass with fewer lanes
+// uses the front of the buffers), never cleared: every pass writes every row of its lanes
+// before any read.  Freeing and re-allocating a large buffer is slow on this platform
+// (the driver wipes freed memory before handing it out again: ~4 s for 100-150 GB,
+// tools/alloc_probe.hip), so callers reserve the largest pass up front (kp_reserve_lanes).
+static int ensure_lanes(kp_plan *p, uint64_t lanes) {
+    if (lanes <= p->lanes_cap) return KP_OK;
+    const kp::host_plan &hp = p->hp;
+    const uint32_t ncap = node_cap_of(hp);
+    dfree(p->d_S);
+    dfree(p->d_nodes);
+    p->d_S = nullptr;
+    p->d_nodes = nullptr;
+    p->lanes_cap = 0;
+    size_t sb = hp.g.nblocks * (size_t)lanes * hp.g.Bpad * 4, nb = (size_t)lanes * ncap * sizeof(kp_node);
+    size_t fr = 0, tot = 0;
+    KP_HIP(hipMemGetInfo(&fr, &tot));
+    if (sb + nb + (256u << 20) > fr)
+        return fail(KP_E_NOMEM, "lanes need " + std::to_string(sb + nb) + " bytes, free " + std::to_string(fr));
+    KP_HIP(hipMalloc(&p->d_S, sb));
+    KP_HIP(hipMalloc(&p->d_nodes, nb));
+    p->lanes_cap = lanes;
+    p->node_cap = ncap;
+    return KP_OK;
+}
+
 template <typename CT>
 static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *root_train, float *root_test,
                     uint64_t *n_leaves) {
@@ -687,24 +713,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     while (threads < KP_DP_MAX_THREADS && threads * KP_IPT < max_level_cells) threads *= 2;
     if (threads * KP_IPT < max_level_cells) return fail(KP_E_ARG, "block level too wide for one workgroup");
     // lane storage: scores, and the backtrack node pool
-    const uint32_t ncap = node_cap_of(hp);
-    if (Ltot > p->lanes_cap) {
-        dfree(p->d_S);
-        dfree(p->d_nodes);
-        p->d_S = nullptr;
-        p->d_nodes = nullptr;
-        p->lanes_cap = 0;
-        size_t sb = g.nblocks * (size_t)Ltot * g.Bpad * 4, nb = (size_t)Ltot * ncap * sizeof(kp_node);
-        size_t fr = 0, tot = 0;
-        KP_HIP(hipMemGetInfo(&fr, &tot));
-        if (sb + nb + (256u << 20) > fr)
-            return fail(KP_E_NOMEM, "lanes need " + std::to_string(sb + nb) + " bytes, free " + std::to_string(fr));
-        KP_HIP(hipMalloc(&p->d_S, sb));
-        KP_HIP(hipMalloc(&p->d_nodes, nb));
-        KP_HIP(hipMemsetAsync(p->d_S, 0, sb, c->stream));
-        p->lanes_cap = Ltot;
-        p->node_cap = ncap;
-    }
+    if (int rc = ensure_lanes(p, Ltot)) return rc;
     if (Ltot > p->small_cap || dg.size() > p->small_cap) {
         void *bufs[] = {p->d_groups, p->d_lanegrp, p->d_rtrain, p->d_rtest, p->d_nleaves,
                         p->d_bad,    p->d_cnt,     p->d_dend,   p->d_leaves};
@@ -899,6 +908,18 @@ int kp_pass(kp_plan *p, const kp_group *groups, int n_groups, float *root_train,
     KP_HIP(hipSetDevice(p->ctx->device));
     if (p->ct_bytes == 4) return run_pass<uint32_t>(p, groups, n_groups, root_train, root_test, n_leaves);
     return run_pass<uint64_t>(p, groups, n_groups, root_train, root_test, n_leaves);
+}
+
+int kp_reserve_lanes(kp_plan *p, uint32_t lanes) {
+    if (!p) return fail(KP_E_ARG, "null plan");
+    KP_HIP(hipSetDevice(p->ctx->device));
+    const uint64_t had = p->lanes_cap;
+    if (int rc = ensure_lanes(p, lanes)) return rc;
+    if (p->lanes_cap != had) {  // fault the new pages in now rather than in the first pass
+        KP_HIP(hipMemsetAsync(p->d_S, 0, p->hp.g.nblocks * (size_t)p->lanes_cap * p->hp.g.Bpad * 4, p->ctx->stream));
+        KP_HIP(hipStreamSynchronize(p->ctx->stream));
+    }
+    return KP_OK;
 }
 
 int kp_last_pass_stats(const kp_plan *p, kp_pass_stats *out) {

@@ -58,7 +58,7 @@ class KPPassStats(ctypes.Structure):
 
 
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
-           "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_pass", "kp_last_pass_stats",
+           "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_pass", "kp_reserve_lanes", "kp_last_pass_stats",
            "kp_fit_leaves", "kp_dump_lane", "kp_fold_split", "kp_kmer_parse", "kp_kmer_table_info",
            "kp_kmer_table_copy", "kp_kmer_table_free"]
 
@@ -95,6 +95,7 @@ def load():
         L.kp_set_counts.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
         L.kp_pass.argtypes = [vp, ctypes.POINTER(KPGroup), ctypes.c_int, vp, vp, vp]
         L.kp_last_pass_stats.argtypes = [vp, ctypes.POINTER(KPPassStats)]
+        L.kp_reserve_lanes.argtypes = [vp, ctypes.c_uint32]
         L.kp_fit_leaves.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u64p]
         L.kp_dump_lane.argtypes = [vp, ctypes.c_uint32, vp, vp]
         L.kp_fold_split.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_int, vp]
@@ -235,6 +236,7 @@ class Plan:
         self.nf = None
         self.itype = None
         self.last_lanes = 0
+        self.lanes_held = 0  # lanes the device buffers hold (they only grow)
 
     def set_counts(self, M, U):
         """Fold counts ``[n_kmers, nf]`` (uint32/uint64) in KmerEnumeration order."""
@@ -274,7 +276,13 @@ class Plan:
         nlv = np.zeros(nl, np.uint64)
         _check(load().kp_pass(self._h, arr, len(groups), _ptr(rt), _ptr(re), _ptr(nlv)))
         self.last_lanes = nl
+        self.lanes_held = max(self.lanes_held, nl)
         return rt, re, nlv
+
+    def reserve(self, lanes):
+        """Allocate the per-lane buffers for ``lanes`` lanes now (kp_reserve_lanes)."""
+        _check(load().kp_reserve_lanes(self._h, int(lanes)))
+        self.lanes_held = max(self.lanes_held, int(lanes))
 
     def stats(self):
         s = KPPassStats()
@@ -298,8 +306,8 @@ class Plan:
     def lanes_that_fit(self, reserve=2 << 30):
         fr, _ = self.device.mem()
         per = self.info["bytes_per_lane"]
-        # buffers of the current pass are reused: count them as available
-        held = self.last_lanes * per
+        # the lane buffers already held are reused: count them as available
+        held = self.lanes_held * per
         return max(0, int((fr + held - reserve) // per))
 
     def close(self):
@@ -433,7 +441,9 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
             if chunk:
                 plan = get_plan(dev, gen_pat, max_block)
                 plan.set_counts(M, U)
-                for pas in pack_passes(chunk, plan.lanes_that_fit()):
+                passes = pack_passes(chunk, plan.lanes_that_fit())
+                plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))  # one allocation
+                for pas in passes:
                     outs.append(plan.run(pas))
             if outs:
                 results[slot] = tuple(np.concatenate([o[i] for o in outs]) for i in range(3))

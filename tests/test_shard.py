@@ -114,6 +114,9 @@ def test_engine_run_groups_lane_granular_over_devices(monkeypatch):
         def lanes_that_fit(self):
             return 7
 
+        def reserve(self, lanes):
+            assert lanes <= 7
+
         def run(self, groups):
             lanes = [(g[0], g[1], c) for g in groups for c in g[3]]
             for ln in lanes:

@@ -174,6 +174,29 @@ int main(int argc, char **argv) {
             std::sort(kv.begin(), kv.end());
             const uint64_t G = (uint64_t)std::max(param, 1);
             for (uint64_t q = 0; q < nb; ++q) xs[(q / G) & 7u].push_back(kv[q].second);
+        } else if (sched == "chunk3") {
+            // plan order (perm fastest-first: kh-1, kh-2, ...), but the third-fastest
+            // position is cut into chunks of `param` digits, the chunk coordinate varying
+            // just slower than the third position's loop... i.e. key =
+            // (slow positions, chunk(p3), p3, p2, p1)
+            std::vector<std::pair<std::vector<uint32_t>, uint64_t>> kv(nb);
+            const int p1 = g.kh - 1, p2 = g.kh - 2, p3 = g.kh - 3;
+            for (uint64_t e = 0; e < nb; ++e) {
+                const uint64_t h = P.hlist[b0 + e];
+                std::vector<uint32_t> key;
+                for (int i = 0; i < g.kh; ++i)
+                    if (i != p1 && i != p2 && i != p3) key.push_back(kp_high_digit(g, h, i));
+                std::reverse(key.begin(), key.end());  // earlier positions slower? keep plan: M slowest
+                const uint32_t d3 = kp_high_digit(g, h, p3);
+                key.push_back(d3 / (uint32_t)param);
+                key.push_back(d3);
+                key.push_back(kp_high_digit(g, h, p2));
+                key.push_back(kp_high_digit(g, h, p1));
+                kv[e] = {key, h};
+            }
+            std::stable_sort(kv.begin(), kv.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+            const uint64_t G = 8;
+            for (uint64_t q = 0; q < nb; ++q) xs[(q / G) & 7u].push_back(kv[q].second);
         } else {
             fprintf(stderr, "unknown schedule\n");
             return 2;
