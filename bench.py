@@ -201,16 +201,39 @@ def cv_shares(prep, world, cap):
     return [pack_passes(rank_groups(prep["groups"], r, world), cap) for r in range(world)]
 
 
-def full_cv(plan, prep, gen_pat, rank, world, cap, model_world=8):
-    """The whole grid x folds as the CV driver runs it, on the already-built plan (its
-    table upload and lane allocation are timed at start-up, ``t_plan`` / ``t_reserve``):
-    fold split (host C++), count tables, this rank's lane-granular share of the passes,
-    root read-out.  At world 1 it also runs the shares the ``model_world`` ranks of an
-    8-GPU job would get, one after the other, and models that job's wall-clock as the
-    serial setup plus the slowest share (there is no data-path collective)."""
+def full_cv(prep, gen_pat, max_block, rank, world, model_world=8):
+    """The whole grid x folds as the CV driver runs it in a fresh process (this leg runs
+    first): the plan's tables and one lane allocation for the largest pass are set up on
+    the GPU while the host draws the fold split (as cv_roots does), then count tables,
+    this rank's lane-granular share of the passes, root read-out.  At world 1 it also runs
+    the shares the ``model_world`` ranks of an 8-GPU job would get, one after the other,
+    and models that job's wall-clock as the serial setup plus the slowest share (there is
+    no data-path collective).  Returns (record, plan, cap)."""
+    import threading
     from kmerpapa_amd.CV_tools import fold_tables as _ft
+    box = {}
     t0 = time.perf_counter()
+
+    def setup_gpu():
+        try:
+            plan = engine.get_plan(prep["device"], gen_pat, max_block)
+            box["t_plan"] = time.perf_counter() - t0
+            cap = min(plan.lanes_that_fit(), 8)
+            worlds = (world, model_world) if world == 1 else (world,)
+            most = max([len(prep["groups"][0][3])] + [sum(len(g[3]) for g in p) for w in worlds
+                                                      for passes in cv_shares(prep, w, cap) for p in passes])
+            plan.reserve(most)
+            box.update(plan=plan, cap=cap, most=most, t_gpu=time.perf_counter() - t0)
+        except Exception as e:  # re-raised in the caller's thread
+            box["error"] = e
+    th = threading.Thread(target=setup_gpu)
+    th.start()
     contexts, Mf, Uf = _ft(prep["ctx"], prep["nfolds"], np.random.RandomState(1), prep["itype"])
+    t_split = time.perf_counter() - t0
+    th.join()
+    if "error" in box:
+        raise box["error"]
+    plan, cap = box["plan"], box["cap"]
     Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, plan.info["n_kmers"], prep["itype"])
     plan.set_counts(Mk, Uk)
     t_setup = time.perf_counter() - t0
@@ -221,15 +244,15 @@ def full_cv(plan, prep, gen_pat, rank, world, cap, model_world=8):
             plan.run(p)
         return time.perf_counter() - ts, sum(len(g[3]) for p in passes for g in p)
     t_mine, lanes_mine = share(cv_shares(prep, world, cap)[rank])
-    fixed = prep["t_plan"] + prep["t_reserve"]
-    out = {"wall_s": fixed + t_setup + t_mine, "plan_and_alloc_s": fixed, "fold_split_and_counts_s": t_setup,
+    out = {"wall_s": t_setup + t_mine, "setup_s": t_setup, "fold_split_s": t_split,
+           "gpu_setup_s": box["t_gpu"], "plan_s": box["t_plan"], "reserved_lanes": box["most"],
            "passes_s": t_mine, "lanes": lanes_mine}
     if world == 1 and model_world > 1:
         shares = [share(p) for p in cv_shares(prep, model_world, cap)]
         out["model"] = {"world": model_world, "share_s": [round(x[0], 4) for x in shares],
                         "share_lanes": [x[1] for x in shares],
-                        "wall_s": fixed + t_setup + max(x[0] for x in shares)}
-    return out
+                        "wall_s": t_setup + max(x[0] for x in shares)}
+    return out, plan, cap
 
 
 def main():
@@ -260,28 +283,7 @@ def main():
     prep = prepare(gen_pat, alphas=cfg["alphas"], penalties=cfg["penalties"], nfolds=cfg["nfolds"])
     ndev = engine.device_count()
     prep["device"] = local % max(1, ndev)  # one GPU per rank (several ranks per GPU only in rehearsals)
-    dev = engine.get_device(prep["device"])
-    t0 = time.perf_counter()
-    plan = engine.get_plan(dev.device, gen_pat, a.max_block)
-    prep["t_plan"] = time.perf_counter() - t0
-    plan.set_counts(prep["Mk"], prep["Uk"])
-    t_setup = time.perf_counter() - t0
     groups = prep["groups"]
-    # one allocation for the largest pass of the run (re-allocating large buffers is slow)
-    cap = min(plan.lanes_that_fit(), 8)
-    most = max([len(groups[0][3])] + [sum(len(g[3]) for g in p) for w in (world, 8) if not a.no_full_cv
-                                      for passes in cv_shares(prep, w, cap) for p in passes])
-    t0 = time.perf_counter()
-    plan.reserve(most)
-    prep["t_reserve"] = time.perf_counter() - t0
-
-    def step(s):
-        g = groups[(s * world + rank) % len(groups)]
-        plan.run([g])
-        return plan.stats()
-
-    for s in range(a.warmup):
-        step(s)
 
     def barrier():
         if dist is not None:
@@ -294,6 +296,28 @@ def main():
         t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
+
+    # BASELINE.json's second metric first, as a fresh process would run it: the full grid CV
+    # wall-clock (fold split, GPU setup, passes, root read-out), max over ranks; at N=1 also
+    # the modelled 8-GPU wall-clock
+    cv = None
+    if not a.no_full_cv:
+        barrier()
+        cv, plan, cap = full_cv(prep, gen_pat, a.max_block, rank, world)
+        cv["wall_s"] = max_over_ranks(cv["wall_s"])
+        plan.set_counts(prep["Mk"], prep["Uk"])
+    else:
+        plan = engine.get_plan(prep["device"], gen_pat, a.max_block)
+        plan.set_counts(prep["Mk"], prep["Uk"])
+        plan.reserve(len(groups[0][3]))
+
+    def step(s):
+        g = groups[(s * world + rank) % len(groups)]
+        plan.run([g])
+        return plan.stats()
+
+    for s in range(a.warmup):
+        step(s)
 
     barrier()
     t_start = time.perf_counter()
@@ -314,13 +338,6 @@ def main():
     tag = engine.kernel_tag()
     tr = committed_traffic(gen_pat, lanes, tag)
 
-    # BASELINE.json's second metric: the full grid CV wall-clock (fold split, setup, passes,
-    # root read-out), max over ranks; at N=1 also the modelled 8-GPU wall-clock
-    cv = None
-    if not a.no_full_cv:
-        barrier()
-        cv = full_cv(plan, prep, gen_pat, rank, world, cap)
-        cv["wall_s"] = max_over_ranks(cv["wall_s"])
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
         roof = {"bound": "hbm", "achieved": must / dp_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
@@ -373,10 +390,7 @@ def main():
             "cv_full_grid_wall_s": cv["wall_s"] if cv else None,
             "cv_full_grid": cv,
             "fold_split_s": prep["t_fold_s"],
-            "setup_s": t_setup,
-            "plan_s": prep["t_plan"],
-            "reserve_s": prep["t_reserve"],
-            "reserved_lanes": most,
+
             "kernel_tag": tag,
         }
         if cv and "model" in cv:

@@ -14,6 +14,7 @@ the numpy<2 float64 sum of the root test values (:159, :171), the strict-"<" sel
 in alpha-major order (:165-177).
 """
 import sys
+import threading
 
 import numpy as np
 
@@ -54,10 +55,32 @@ def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, ity
     n_kmers = generality(gen_pat)
     mult = None
     prevM = prevU = None
+    prepare = getattr(run_groups, "prepare", None)
     for it in range(iterations):
         if verbose > 0 and iterations > 1:
             print('CV Iteration', it, file=sys.stderr)
-        contexts, Mf, Uf = fold_tables(contextD, nfolds, prng, itype)
+        th = None
+        if prepare is not None and it == 0:
+            # the GPUs' lattice tables and lane buffers are set up while the host draws the
+            # fold split (the native split releases the GIL); only lane counts matter here
+            shape = [(f, a, 1.0, list(penalties[c0:c0 + engine.MAX_GROUP_LANES]))
+                     for a in alphas for f in range(nfolds) for c0 in range(0, nc, engine.MAX_GROUP_LANES)]
+            box = {}
+
+            def _prep():
+                try:
+                    prepare(gen_pat, shape, devices=devices, max_block=max_block)
+                except Exception as e:  # re-raised below, in the caller's thread
+                    box["error"] = e
+            th = threading.Thread(target=_prep)
+            th.start()
+        try:
+            contexts, Mf, Uf = fold_tables(contextD, nfolds, prng, itype)
+        finally:
+            if th is not None:
+                th.join()
+        if th is not None and "error" in box:
+            raise box["error"]
         if verbose > 0:
             print('CV sampling DONE', file=sys.stderr)
         Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, n_kmers, itype)

@@ -416,6 +416,31 @@ def release_all():
         _plans.clear()
 
 
+def _device_shares(groups, devices):
+    from .shard import rank_groups
+    return [rank_groups(groups, slot, len(devices)) for slot in range(len(devices))]
+
+
+def prepare_groups(gen_pat, groups, devices=None, max_block=0):
+    """Everything ``run_groups`` needs before the counts exist: each GPU's plan (lattice
+    tables uploaded) and one allocation for its largest pass.  Only the lane counts of
+    ``groups`` matter (folds, alphas and betas may be placeholders), so a caller can run
+    this while the host draws the fold split (CV_tools.fold_tables drops the GIL)."""
+    devices = list(dict.fromkeys(devices if devices is not None else visible_devices()[:1]))
+
+    def prep(dev, chunk):
+        if chunk:
+            plan = get_plan(dev, gen_pat, max_block)
+            passes = pack_passes(chunk, plan.lanes_that_fit())
+            plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
+    threads = [threading.Thread(target=prep, args=(dev, chunk))
+               for dev, chunk in zip(devices, _device_shares(groups, devices))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+
+
 def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     """Run every lane group over the lattice of ``gen_pat`` on the given GPUs.
 
@@ -430,8 +455,8 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     devices = list(dict.fromkeys(devices))  # one host thread per GPU: a device's plan is not shared
     if not devices:
         raise KPError(-3, "no GPU visible")
-    from .shard import rank_groups
     nd = len(devices)
+    shares = _device_shares(groups, devices)  # slots in order = lanes in order
     results = [None] * nd
     errors = []
 
@@ -454,7 +479,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
 
     threads = []
     for slot, dev in enumerate(devices):
-        chunk = rank_groups(groups, slot, nd)  # slots in order = lanes in order
+        chunk = shares[slot]
         if nd == 1:
             work(slot, dev, chunk)
         else:
@@ -466,3 +491,6 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     if errors:
         raise errors[0]
     return tuple(np.concatenate([r[i] for r in results]) for i in range(3))
+
+
+run_groups.prepare = prepare_groups

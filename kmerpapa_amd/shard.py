@@ -55,6 +55,12 @@ def sharded_run_groups(run_groups, rank, world, all_gather, devices=None):
     """
     fixed = devices
 
+    def prepare(gen_pat, groups, devices=None, max_block=0):
+        inner = getattr(run_groups, "prepare", None)
+        mine = rank_groups(groups, rank, world)
+        if inner is not None and mine:
+            inner(gen_pat, mine, devices=fixed if fixed is not None else devices, max_block=max_block)
+
     def run(gen_pat, M, U, groups, devices=None, max_block=0):
         mine = rank_groups(groups, rank, world)
         if mine:
@@ -64,6 +70,7 @@ def sharded_run_groups(run_groups, rank, world, all_gather, devices=None):
             rt, re, nl = np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(0, np.uint64)
         parts = all_gather((np.asarray(rt), np.asarray(re), np.asarray(nl)))
         return tuple(np.concatenate([p[i] for p in parts]) for i in range(3))
+    run.prepare = prepare
     return run
 
 
