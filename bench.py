@@ -218,7 +218,7 @@ def full_cv(prep, gen_pat, max_block, rank, world, model_world=8):
         try:
             plan = engine.get_plan(prep["device"], gen_pat, max_block)
             box["t_plan"] = time.perf_counter() - t0
-            cap = min(plan.lanes_that_fit(), 8)
+            cap = engine.pass_cap(prep["groups"], plan.lanes_that_fit())
             worlds = (world, model_world) if world == 1 else (world,)
             most = max([len(prep["groups"][0][3])] + [sum(len(g[3]) for g in p) for w in worlds
                                                       for passes in cv_shares(prep, w, cap) for p in passes])

@@ -366,6 +366,13 @@ def counts_in_kmer_order(gen_pat, contexts, M, U, n_kmers, itype):
     return outM, outU
 
 
+def pass_cap(groups, fit):
+    """Lanes per pass: the largest group, if it fits.  Passes with more lanes are not faster
+    per lane (each (alpha, fold) group is its own set of workgroups), but need more HBM,
+    and a large allocation can be slow (freed HBM is wiped before reuse)."""
+    return min(fit, max([len(g[3]) for g in groups] or [1]))
+
+
 def pack_passes(groups, max_lanes):
     """Split a group list into passes of at most ``max_lanes`` lanes (order kept)."""
     if max_lanes < 1:
@@ -431,7 +438,7 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0):
     def prep(dev, chunk):
         if chunk:
             plan = get_plan(dev, gen_pat, max_block)
-            passes = pack_passes(chunk, plan.lanes_that_fit())
+            passes = pack_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
             plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
     threads = [threading.Thread(target=prep, args=(dev, chunk))
                for dev, chunk in zip(devices, _device_shares(groups, devices))]
@@ -466,7 +473,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
             if chunk:
                 plan = get_plan(dev, gen_pat, max_block)
                 plan.set_counts(M, U)
-                passes = pack_passes(chunk, plan.lanes_that_fit())
+                passes = pack_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
                 plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))  # one allocation
                 for pas in passes:
                     outs.append(plan.run(pas))

@@ -10,11 +10,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from kmerpapa_amd import engine  # noqa: E402
 
-comps = [[5], [1], [2], [3], [4], [5, 1], [5, 5], [4, 4], [3, 3, 2], [5, 3]]
+comps = [[5], [1], [2], [3], [4], [5, 1], [4, 4], [3, 3, 2], [5, 3]]
 prep = bench.prepare("NNNNMNNNN")
 plan = engine.get_plan(0, "NNNNMNNNN")
 plan.set_counts(prep["Mk"], prep["Uk"])
-plan.reserve(10)
+plan.reserve(8)
 g = prep["groups"]
 plan.run([g[0]])  # warm
 for comp in comps:
