@@ -43,6 +43,7 @@ struct kp_dp_params {
                 // 1 = XCD-contiguous (7 % slower), 0 = hardware round-robin
     int lanesplit;  // split a cell's lanes over threads on narrow levels (KP_LANE_SPLIT=0 disables)
     int ntstore;    // 1 = score rows stored non-temporally (default; KP_NT_STORE=0 for plain stores)
+    uint32_t ntmask;  // high positions whose child rows are loaded non-temporally (bit i = high position i)
     unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
     int dbg;  // -DKP_ABLATION builds only (KP_DEBUG_SKIP, wrong results; always 0 otherwise): 1 = skip gather, 2 = skip level phase,
               // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier
@@ -88,14 +89,58 @@ __device__ inline void kp_min4v(float4 &best, const float4 a, const float4 b) {
     best.w = fminf(best.w, a.w + b.w);
 }
 
+// one child-row float4 load; NT = non-temporal (no cache allocation, for rows that will
+// not be read again soon)
+template <bool NT>
+__device__ inline float4 kp_ld4(const float *p) {
+    if (NT) {
+        typedef float kp_f4v __attribute__((ext_vector_type(4)));
+        const kp_f4v v = __builtin_nontemporal_load(reinterpret_cast<const kp_f4v *>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    }
+    return *reinterpret_cast<const float4 *>(p);
+}
+
+// pairs p0..p1 of the block's high split pairs, NI items per thread, PU pairs per step
+template <int NI, int PU, bool NT>
+__device__ inline void kp_gather_range(const kp_dp_params &P, const kp_hpair *hp, int p0, int p1,
+                                       const uint32_t *o, float4 *best) {
+    int p = p0;
+    for (; p + PU <= p1; p += PU) {
+        const float *r[2 * PU];
+#pragma unroll
+        for (int q = 0; q < PU; ++q) {
+            r[2 * q] = P.S + kp_rfl64(hp[p + q].h1);
+            r[2 * q + 1] = P.S + kp_rfl64(hp[p + q].h2);
+        }
+        float4 v[NI][2 * PU];
+#pragma unroll
+        for (int q = 0; q < 2 * PU; ++q)
+#pragma unroll
+            for (int i = 0; i < NI; ++i) v[i][q] = kp_ld4<NT>(r[q] + o[i]);
+#pragma unroll
+        for (int q = 0; q < PU; ++q)
+#pragma unroll
+            for (int i = 0; i < NI; ++i) kp_min4v(best[i], v[i][2 * q], v[i][2 * q + 1]);
+    }
+    for (; p < p1; ++p) {
+        const float *ra = P.S + kp_rfl64(hp[p].h1), *rb = P.S + kp_rfl64(hp[p].h2);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) kp_min4v(best[i], kp_ld4<NT>(ra + o[i]), kp_ld4<NT>(rb + o[i]));
+    }
+}
+
 // Gather phase of one block: st[cell][lane] = min over the block's high split pairs of
 // S[child1] + S[child2], for the NL lanes.  Items are float4 runs (4 cells of one lane);
 // each thread takes NI items at a time (NI * 2 * min(np, PU) row loads in flight).  A
 // pair's child-row offsets are workgroup-uniform: read into SGPRs, so each load is a
-// scalar base plus a 32-bit lane offset.  Slot B (padding) becomes +inf: the cell that
-// padded pair lists point at (kp_dp_cell_list).
+// scalar base plus a 32-bit lane offset.  Pairs 0..nnt-1 (the plan's slowest-varying
+// high positions, whose child rows are not re-read while they could still be cached) use
+// non-temporal loads.  Slot B (padding) becomes +inf: the cell that padded pair lists
+// point at (kp_dp_cell_list).
 template <int NL, int NI, int PU = 4>
-__device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp, int np, uint32_t lane0, float *st) {
+__device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp, int np, int nnt, uint32_t lane0,
+                                       float *st) {
     const kp_geom &g = P.g;
     const uint32_t Bpad = g.Bpad, nch = Bpad / 4, nitems = (uint32_t)NL * nch;
     const float inf = __builtin_huge_valf();
@@ -108,31 +153,8 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
             o[i] = (lane0 + it[i] / nch) * Bpad + 4 * (it[i] % nch);
             best[i] = make_float4(inf, inf, inf, inf);
         }
-        int p = 0;
-        for (; p + PU <= np; p += PU) {
-            const float *r[2 * PU];
-#pragma unroll
-            for (int q = 0; q < PU; ++q) {
-                r[2 * q] = P.S + kp_rfl64(hp[p + q].h1);
-                r[2 * q + 1] = P.S + kp_rfl64(hp[p + q].h2);
-            }
-            float4 v[NI][2 * PU];
-#pragma unroll
-            for (int q = 0; q < 2 * PU; ++q)
-#pragma unroll
-                for (int i = 0; i < NI; ++i) v[i][q] = *reinterpret_cast<const float4 *>(r[q] + o[i]);
-#pragma unroll
-            for (int q = 0; q < PU; ++q)
-#pragma unroll
-                for (int i = 0; i < NI; ++i) kp_min4v(best[i], v[i][2 * q], v[i][2 * q + 1]);
-        }
-        for (; p < np; ++p) {
-            const float *ra = P.S + kp_rfl64(hp[p].h1), *rb = P.S + kp_rfl64(hp[p].h2);
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-                kp_min4v(best[i], *reinterpret_cast<const float4 *>(ra + o[i]),
-                         *reinterpret_cast<const float4 *>(rb + o[i]));
-        }
+        if (nnt > 0) kp_gather_range<NI, PU, true>(P, hp, 0, nnt, o, best);
+        kp_gather_range<NI, PU, false>(P, hp, nnt, np, o, best);
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             if (i > 0 && it[i] == it0) break;
@@ -199,23 +221,31 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     // plan (no 64-bit division), counts per position are uniform loads, and wave 0 writes
     // one pair per lane
     const uint64_t hd = P.T.hdig[P.hbase + widx];
-    int np = 0;
+    int np = 0, nnt = 0;
     if (!KP_SKIP(P, 1))
-        for (int i = 0; i < g.kh; ++i) np += P.T.tabs[g.t + i].np[(hd >> (4 * i)) & 15u];
+        for (int i = 0; i < g.kh; ++i) {
+            const int npi = P.T.tabs[g.t + i].np[(hd >> (4 * i)) & 15u];
+            np += npi;
+            if ((P.ntmask >> i) & 1u) nnt += npi;
+        }
     const uint64_t rowstride = (uint64_t)g.Ltot * Bpad;
     for (int p = (int)threadIdx.x; threadIdx.x < 64 && p < np; p += 64) {  // wave 0
-        int rem = p, i = 0;
+        // pair p in scan order; slot: the non-temporal positions' pairs first (the sweep
+        // only takes a min, so pair order does not matter here)
+        int rem = p, i = 0, before_nt = 0, before_t = 0;
         uint32_t d = 0;
         for (; i < g.kh; ++i) {
             d = (uint32_t)(hd >> (4 * i)) & 15u;
             const int npi = P.T.tabs[g.t + i].np[d];
             if (rem < npi) break;
             rem -= npi;
+            if ((P.ntmask >> i) & 1u) before_nt += npi; else before_t += npi;
         }
+        const int slot = ((P.ntmask >> i) & 1u) ? before_nt + rem : nnt + before_t + rem;
         const kp_postab &T = P.T.tabs[g.t + i];
-        hp[p].h1 = (h - (uint64_t)(d - T.pa[d][rem]) * g.hcg[i]) * rowstride;  // child rows as element
-        hp[p].h2 = (h - (uint64_t)(d - T.pb[d][rem]) * g.hcg[i]) * rowstride;  // offsets of lane 0
-        hp[p].code = (uint32_t)(((g.t + i) << 3) | rem);
+        hp[slot].h1 = (h - (uint64_t)(d - T.pa[d][rem]) * g.hcg[i]) * rowstride;  // child rows as element
+        hp[slot].h2 = (h - (uint64_t)(d - T.pb[d][rem]) * g.hcg[i]) * rowstride;  // offsets of lane 0
+        hp[slot].code = (uint32_t)(((g.t + i) << 3) | rem);
     }
     for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 16u; e += blockDim.x) lm[e] = P.T.lowmask[e];
     __syncthreads();  // lm is read by every thread below
@@ -230,7 +260,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     // ---- gather: high-position splits, as whole child-block rows (value only) ----
     // four float4 items per thread at a time, two pairs per step: 16 row loads in flight
     // per thread even when the block has few pairs (measured best of 1-4 items x 1-4 pairs)
-    kp_gather_items<NL, 4, 2>(P, hp, np, lane0, st);
+    kp_gather_items<NL, 4, 2>(P, hp, np, nnt, lane0, st);
     __syncthreads();
     KP_STAMP(1);
 

@@ -756,6 +756,13 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 8;
     P.lanesplit = getenv("KP_LANE_SPLIT") ? atoi(getenv("KP_LANE_SPLIT")) : 1;
     P.ntstore = getenv("KP_NT_STORE") ? atoi(getenv("KP_NT_STORE")) : 1;
+    // child rows along the KP_NT_SLOW slowest-varying high positions of the block order
+    // are read non-temporally: under that order they are not re-read while still cached
+    {
+        const int nslow = getenv("KP_NT_SLOW") ? atoi(getenv("KP_NT_SLOW")) : 0;
+        P.ntmask = 0;
+        for (int q = 0; q < nslow && q < (int)hp.perm.size(); ++q) P.ntmask |= 1u << hp.perm[hp.perm.size() - 1 - q];
+    }
     P.stamps = nullptr;
 #ifdef KP_STAMPS
     static unsigned long long *d_stamps = nullptr;

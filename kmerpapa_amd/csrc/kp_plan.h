@@ -56,6 +56,7 @@ struct host_plan {
     std::vector<uint32_t> hlist;       // [nblocks] blocks sorted by high level
     std::vector<uint64_t> hdig;        // [nblocks] their high digits, 4 bits per high position
     std::vector<uint64_t> hoff;        // [hmax + 2]
+    std::vector<int> perm;             // high positions of the block order, fastest first
     uint32_t kh_nuc_weight = 0;
     // algorithmic accounting: split pairs summed over all cells
     double pairs_total = 0.0, pairs_low = 0.0, pairs_high = 0.0;
@@ -300,6 +301,7 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
         }
         for (int i = g.kh - 1; i >= 0; --i)  // complete a partial explicit permutation
             if (std::find(perm.begin(), perm.end(), i) == perm.end()) perm.push_back(i);
+        P.perm = perm;
         std::vector<uint64_t> fill(P.hoff.begin(), P.hoff.end() - 1);
         // KP_BLOCK_TILE=T (experiment): tiles of T digits per high position, the digits
         // inside a tile (perm order) varying faster than the tile coordinates

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <list>
+#include <set>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -29,6 +30,7 @@ struct LRU {
     std::list<uint64_t> order;
     std::unordered_map<uint64_t, std::list<uint64_t>::iterator> pos;
     explicit LRU(size_t c) : cap(c) {}
+    bool peek(uint64_t key) const { return pos.count(key) > 0; }
     bool touch(uint64_t key) {  // true = hit
         auto it = pos.find(key);
         if (it != pos.end()) {
@@ -64,6 +66,14 @@ int main(int argc, char **argv) {
     const size_t l2_rows = argc > 5 ? (size_t)atol(argv[5]) : (size_t)(4.0 * 1048576 / row_bytes);
     const size_t mall_rows = argc > 6 ? (size_t)atol(argv[6]) : (size_t)(256.0 * 1048576 / row_bytes);
     std::vector<LRU> l2(8, LRU(l2_rows));
+    // KP_NT_POS="a,b,..." = high positions (0-based among high positions) read non-temporally
+    std::set<int> slow_nt;
+    if (const char *e = getenv("KP_NT_POS"))
+        for (const char *c = e; *c;) {
+            slow_nt.insert(atoi(c));
+            while (*c >= '0' && *c <= '9') ++c;
+            while (*c && (*c < '0' || *c > '9')) ++c;
+        }
     LRU mall(mall_rows);
     uint64_t reads = 0, l2miss = 0, mallmiss = 0, writes = 0, distinct = 0;
     for (int H = 0; H <= P.hmax; ++H) {
@@ -218,14 +228,24 @@ int main(int argc, char **argv) {
                 if (s >= xs[x].size()) continue;
                 const uint64_t h = xs[x][s];
                 const int np = kp_high_pairs(g, P.tabs.data(), h, hp);
-                for (int p = 0; p < np; ++p)
+                for (int p = 0; p < np; ++p) {
+                    // high position of the pair (code = position << 3 | pair); its rank in the
+                    // plan order: positions kh-1, kh-2, ... are fastest (M last)
+                    const int pos = (int)(hp[p].code >> 3) - g.t;
+                    const bool nt = slow_nt.count(pos) > 0;
                     for (uint64_t c : {hp[p].h1, hp[p].h2}) {
                         ++reads;
-                        if (!l2[x].touch(c)) {
+                        if (nt) {  // non-temporal: hits where present, allocates nowhere
+                            if (!l2[x].peek(c)) {
+                                ++l2miss;
+                                if (!mall.peek(c)) ++mallmiss;
+                            }
+                        } else if (!l2[x].touch(c)) {
                             ++l2miss;
                             if (!mall.touch(c)) ++mallmiss;
                         }
                     }
+                }
                 ++writes;
                 l2[x].touch(h);  // stores keep the line in the XCD's L2 (nt too)
             }
