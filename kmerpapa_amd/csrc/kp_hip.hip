@@ -757,9 +757,11 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.lanesplit = getenv("KP_LANE_SPLIT") ? atoi(getenv("KP_LANE_SPLIT")) : 1;
     P.ntstore = getenv("KP_NT_STORE") ? atoi(getenv("KP_NT_STORE")) : 1;
     // child rows along the KP_NT_SLOW slowest-varying high positions of the block order
-    // are read non-temporally: under that order they are not re-read while still cached
+    // (default 3) are read non-temporally: under that order they are not re-read while
+    // still in the Infinity Cache, so they no longer evict the rows of the fast positions
+    // that are (9-mer pass 403-408 -> 397-398 ms; 2: 399-400, 4: 417)
     {
-        const int nslow = getenv("KP_NT_SLOW") ? atoi(getenv("KP_NT_SLOW")) : 0;
+        const int nslow = getenv("KP_NT_SLOW") ? atoi(getenv("KP_NT_SLOW")) : 3;
         P.ntmask = 0;
         for (int q = 0; q < nslow && q < (int)hp.perm.size(); ++q) P.ntmask |= 1u << hp.perm[hp.perm.size() - 1 - q];
     }
