@@ -413,16 +413,31 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     return T;
 }
 
+// Device memory comes from the stream-ordered allocator (the device's default pool): on
+// this platform a plain hipMalloc of memory another allocation (or process) freed waits
+// for the driver to wipe it, ~30 ms per GB (4-6 s for the 150 GB of a 9-mer pass), while
+// hipMallocAsync returned 150 GB in 0.08 s (tools/alloc_probe.hip).  Every
+// call synchronises before returning, so no queued work ever uses a buffer being freed.
+template <typename T>
+static hipError_t dmalloc(T **p, size_t bytes) {
+    hipError_t e = hipMallocAsync(reinterpret_cast<void **>(p), std::max<size_t>(bytes, 1), nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    return e;
+}
+
 template <typename T>
 static int upload(T **dptr, const std::vector<T> &v) {
     size_t bytes = std::max<size_t>(1, v.size()) * sizeof(T);
-    KP_HIP(hipMalloc(reinterpret_cast<void **>(dptr), bytes));
+    KP_HIP(dmalloc(dptr, bytes));
     if (!v.empty()) KP_HIP(hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     return KP_OK;
 }
 
 static void dfree(void *p) {
-    if (p) (void)hipFree(p);
+    if (p) {
+        (void)hipFreeAsync(p, nullptr);
+        (void)hipStreamSynchronize(nullptr);
+    }
 }
 
 // nodes of one lane's backtrack tree: at most 2 * leaves - 1 <= 2 * n_kmers - 1
@@ -538,8 +553,8 @@ static int run_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers
     g.nf = nf;
     size_t in_bytes = n_kmers * (size_t)nf * sizeof(CT);
     CT *dM = nullptr, *dU = nullptr;
-    KP_HIP(hipMalloc(&dM, in_bytes));
-    KP_HIP(hipMalloc(&dU, in_bytes));
+    KP_HIP(dmalloc(&dM, in_bytes));
+    KP_HIP(dmalloc(&dU, in_bytes));
     KP_HIP(hipMemcpyAsync(dM, M, in_bytes, hipMemcpyHostToDevice, c->stream));
     KP_HIP(hipMemcpyAsync(dU, U, in_bytes, hipMemcpyHostToDevice, c->stream));
     size_t kbytes = g.nblocks * (size_t)g.n_kl * nf * 2 * sizeof(CT);
@@ -555,7 +570,7 @@ static int run_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers
             dfree(dU);
             return fail(KP_E_NOMEM, "count tables need " + std::to_string(kbytes) + " bytes");
         }
-        KP_HIP(hipMalloc(&p->d_K, kbytes));
+        KP_HIP(dmalloc(&p->d_K, kbytes));
     }
     kp_dev_tables T = tables_of(p);
     for (int H = 0; H <= p->hp.hmax; ++H) {
@@ -659,8 +674,8 @@ static int ensure_lanes(kp_plan *p, uint64_t lanes) {
     KP_HIP(hipMemGetInfo(&fr, &tot));
     if (sb + nb + (256u << 20) > fr)
         return fail(KP_E_NOMEM, "lanes need " + std::to_string(sb + nb) + " bytes, free " + std::to_string(fr));
-    KP_HIP(hipMalloc(&p->d_S, sb));
-    KP_HIP(hipMalloc(&p->d_nodes, nb));
+    KP_HIP(dmalloc(&p->d_S, sb));
+    KP_HIP(dmalloc(&p->d_nodes, nb));
     p->lanes_cap = lanes;
     p->node_cap = ncap;
     return KP_OK;
@@ -719,15 +734,15 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
                         p->d_bad,    p->d_cnt,     p->d_dend,   p->d_leaves};
         for (void *b : bufs) dfree(b);
         uint64_t cap = std::max<uint64_t>(Ltot, 64);
-        KP_HIP(hipMalloc(&p->d_groups, cap * sizeof(kp_group_dev)));
-        KP_HIP(hipMalloc(&p->d_lanegrp, cap * sizeof(uint32_t)));
-        KP_HIP(hipMalloc(&p->d_rtrain, cap * sizeof(float)));
-        KP_HIP(hipMalloc(&p->d_rtest, cap * sizeof(float)));
-        KP_HIP(hipMalloc(&p->d_nleaves, cap * sizeof(uint64_t)));
-        KP_HIP(hipMalloc(&p->d_bad, cap * sizeof(uint32_t)));
-        KP_HIP(hipMalloc(&p->d_cnt, cap * sizeof(uint32_t)));
-        KP_HIP(hipMalloc(&p->d_dend, cap * (KP_MAXDEPTH + 1) * sizeof(uint32_t)));
-        KP_HIP(hipMalloc(&p->d_leaves, cap * hp.n_kmers * sizeof(uint64_t)));
+        KP_HIP(dmalloc(&p->d_groups, cap * sizeof(kp_group_dev)));
+        KP_HIP(dmalloc(&p->d_lanegrp, cap * sizeof(uint32_t)));
+        KP_HIP(dmalloc(&p->d_rtrain, cap * sizeof(float)));
+        KP_HIP(dmalloc(&p->d_rtest, cap * sizeof(float)));
+        KP_HIP(dmalloc(&p->d_nleaves, cap * sizeof(uint64_t)));
+        KP_HIP(dmalloc(&p->d_bad, cap * sizeof(uint32_t)));
+        KP_HIP(dmalloc(&p->d_cnt, cap * sizeof(uint32_t)));
+        KP_HIP(dmalloc(&p->d_dend, cap * (KP_MAXDEPTH + 1) * sizeof(uint32_t)));
+        KP_HIP(dmalloc(&p->d_leaves, cap * hp.n_kmers * sizeof(uint64_t)));
         p->small_cap = cap;
     }
     KP_HIP(hipMemcpyAsync(p->d_groups, dg.data(), dg.size() * sizeof(kp_group_dev), hipMemcpyHostToDevice, c->stream));
@@ -768,7 +783,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.stamps = nullptr;
 #ifdef KP_STAMPS
     static unsigned long long *d_stamps = nullptr;
-    if (!d_stamps) KP_HIP(hipMalloc(&d_stamps, 32 * sizeof(unsigned long long)));
+    if (!d_stamps) KP_HIP(dmalloc(&d_stamps, 32 * sizeof(unsigned long long)));
     KP_HIP(hipMemsetAsync(d_stamps, 0, 32 * sizeof(unsigned long long), c->stream));
     P.stamps = d_stamps;
 #endif
@@ -896,7 +911,7 @@ static int run_codes(kp_plan *p, uint32_t lane, uint8_t *code) {
     const kp_group_dev &G = p->last_groups[p->last_lanegrp[lane]];
     const double pen = G.pen[lane - (uint32_t)G.lane0];
     uint8_t *d_code = nullptr;
-    KP_HIP(hipMalloc(&d_code, hp.npat));
+    KP_HIP(dmalloc(&d_code, hp.npat));
     const unsigned nb = (unsigned)std::min<uint64_t>((hp.npat + 255) / 256, 65535);
     hipLaunchKernelGGL(kp_codes_kernel<CT>, dim3(nb), dim3(256), 0, c->stream, g, tables_of(p),
                        reinterpret_cast<const CT *>(p->d_K), p->d_S, G, lane, pen, d_code);

@@ -1,13 +1,14 @@
 // alloc_probe.hip -- how long do very large device allocations take on the MI355X (tool)?
-// Times several allocation APIs for one large size: hipMalloc, hipMalloc again after a
-// hipFree, hipExtMallocWithFlags (default / uncached), hipMallocAsync (default pool, then
-// again after a free), the VMM path (hipMemCreate + hipMemMap), and 16 GB pieces.
+// First dirties the memory (allocate, write and free 200 GB), then times, each followed by
+// a free: one hipMalloc of GB bytes; the same as 8 pieces from 8 host threads at once;
+// hipExtMallocWithFlags(default); hipMallocAsync; and one hipMalloc again.
 // build: hipcc --offload-arch=gfx950 -O2 -o tools/alloc_probe tools/alloc_probe.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
 
 #include <chrono>
+#include <thread>
 #include <vector>
 
 #define CK(x)                                                                 \
@@ -28,87 +29,74 @@ static double now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-static void report(const char *what, double gb, double t_alloc, void *p, size_t bytes) {
-    double t0 = now();
+static void write_all(void *p, size_t bytes) {
     hipLaunchKernelGGL(touch, dim3(8192), dim3(256), 0, 0, (float4 *)p, bytes / 16);
     CK(hipDeviceSynchronize());
-    printf("{\"api\": \"%s\", \"GB\": %.0f, \"alloc_s\": %.4f, \"first_write_s\": %.4f}\n", what, gb, t_alloc,
-           now() - t0);
-    fflush(stdout);
 }
 
 int main(int argc, char **argv) {
-    const double gb = argc > 1 ? atof(argv[1]) : 100.0;
+    const double gb = argc > 1 ? atof(argv[1]) : 150.0;
     const size_t bytes = (size_t)(gb * 1e9) & ~(size_t)((2 << 20) - 1);
     void *p = nullptr;
     double t0;
-    // 1. hipMalloc, twice (the second after a free)
-    for (int rep = 0; rep < 2; ++rep) {
+    {
+        const size_t dirty = (size_t)200e9;
+        t0 = now();
+        CK(hipMalloc(&p, dirty));
+        double t1 = now();
+        write_all(p, dirty);
+        CK(hipFree(p));
+        printf("{\"step\": \"dirty 200 GB\", \"alloc_s\": %.4f, \"write_s\": %.4f}\n", t1 - t0, now() - t1);
+        fflush(stdout);
+    }
+    auto one = [&](const char *name) {
         t0 = now();
         CK(hipMalloc(&p, bytes));
-        report(rep ? "hipMalloc_again" : "hipMalloc", gb, now() - t0, p, bytes);
+        double ta = now() - t0;
         t0 = now();
+        write_all(p, bytes);
+        double tw = now() - t0;
         CK(hipFree(p));
-        printf("{\"api\": \"hipFree\", \"s\": %.4f}\n", now() - t0);
+        printf("{\"step\": \"%s\", \"GB\": %.0f, \"alloc_s\": %.4f, \"first_write_s\": %.4f}\n", name, gb, ta, tw);
+        fflush(stdout);
+    };
+    one("hipMalloc");
+    {
+        const int nt = 8;
+        const size_t piece = (bytes / nt) & ~(size_t)((2 << 20) - 1);
+        std::vector<void *> ps(nt, nullptr);
+        t0 = now();
+        std::vector<std::thread> th;
+        for (int i = 0; i < nt; ++i)
+            th.emplace_back([&, i] {
+                CK(hipSetDevice(0));
+                CK(hipMalloc(&ps[i], piece));
+            });
+        for (auto &t : th) t.join();
+        printf("{\"step\": \"8 threads x hipMalloc\", \"GB\": %.0f, \"alloc_s\": %.4f}\n", gb, now() - t0);
+        fflush(stdout);
+        for (void *q : ps) write_all(q, piece);
+        for (void *q : ps) CK(hipFree(q));
     }
-    // 2. hipExtMallocWithFlags
-    t0 = now();
-    CK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocDefault));
-    report("hipExtMallocWithFlags_default", gb, now() - t0, p, bytes);
-    CK(hipFree(p));
-    t0 = now();
-    CK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached));
-    report("hipExtMallocWithFlags_uncached", gb, now() - t0, p, bytes);
-    CK(hipFree(p));
-    // 3. stream-ordered allocator (default pool), twice
-    hipStream_t s;
-    CK(hipStreamCreate(&s));
-    for (int rep = 0; rep < 2; ++rep) {
+    one("hipMalloc after threads");
+    {
+        t0 = now();
+        CK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocDefault));
+        printf("{\"step\": \"hipExtMallocWithFlags\", \"GB\": %.0f, \"alloc_s\": %.4f}\n", gb, now() - t0);
+        write_all(p, bytes);
+        CK(hipFree(p));
+    }
+    {
+        hipStream_t s;
+        CK(hipStreamCreate(&s));
         t0 = now();
         CK(hipMallocAsync(&p, bytes, s));
         CK(hipStreamSynchronize(s));
-        report(rep ? "hipMallocAsync_again" : "hipMallocAsync", gb, now() - t0, p, bytes);
+        printf("{\"step\": \"hipMallocAsync\", \"GB\": %.0f, \"alloc_s\": %.4f}\n", gb, now() - t0);
+        write_all(p, bytes);
         CK(hipFreeAsync(p, s));
         CK(hipStreamSynchronize(s));
     }
-    // 4. VMM: physical handle + map
-    {
-        hipMemAllocationProp prop = {};
-        prop.type = hipMemAllocationTypePinned;
-        prop.location.type = hipMemLocationTypeDevice;
-        prop.location.id = 0;
-        size_t gran = 0;
-        CK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
-        size_t sz = (bytes + gran - 1) / gran * gran;
-        t0 = now();
-        hipMemGenericAllocationHandle_t h;
-        CK(hipMemCreate(&h, sz, &prop, 0));
-        double t1 = now();
-        void *va = nullptr;
-        CK(hipMemAddressReserve(&va, sz, 0, nullptr, 0));
-        CK(hipMemMap(va, sz, 0, h, 0));
-        hipMemAccessDesc acc = {};
-        acc.location = prop.location;
-        acc.flags = hipMemAccessFlagsProtReadWrite;
-        CK(hipMemSetAccess(va, sz, &acc, 1));
-        printf("{\"api\": \"hipMemCreate\", \"s\": %.4f, \"map_s\": %.4f, \"gran\": %zu}\n", t1 - t0, now() - t1, gran);
-        report("vmm", gb, now() - t0, va, sz);
-        CK(hipMemUnmap(va, sz));
-        CK(hipMemRelease(h));
-        CK(hipMemAddressFree(va, sz));
-    }
-    // 5. 16 GB pieces
-    {
-        const size_t piece = (size_t)16e9 & ~(size_t)((2 << 20) - 1);
-        std::vector<void *> ps;
-        t0 = now();
-        for (size_t done = 0; done < bytes; done += piece) {
-            void *q;
-            CK(hipMalloc(&q, piece));
-            ps.push_back(q);
-        }
-        printf("{\"api\": \"hipMalloc_16GB_pieces\", \"GB\": %.0f, \"alloc_s\": %.4f}\n", gb, now() - t0);
-        for (void *q : ps) CK(hipFree(q));
-    }
+    one("hipMalloc last");
     return 0;
 }
