@@ -413,16 +413,16 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     return T;
 }
 
-// Device memory comes from the stream-ordered allocator (the device's default pool): on
-// this platform a plain hipMalloc of memory another allocation (or process) freed waits
-// for the driver to wipe it, ~30 ms per GB (4-6 s for the 150 GB of a 9-mer pass), while
-// hipMallocAsync returned 150 GB in 0.08 s (tools/alloc_probe.hip).  Every
-// call synchronises before returning, so no queued work ever uses a buffer being freed.
+// Device memory: plain hipMalloc.  On this platform an allocation of HBM that was used
+// before (by this or an earlier process) waits for the driver to wipe it, ~30 ms per GB
+// (4-6 s for the 150 GB of a 9-mer pass; fresh HBM 0.05 s per 100 GB), so the library
+// allocates the large per-lane buffers once (kp_reserve_lanes) and only grows them.  The
+// stream-ordered allocator (hipMallocAsync) skips that wait but is not usable: a 140 GB
+// request served from a freed 100 GB pool block returned memory that did not hold what
+// was written to it (tools/async_check.hip).
 template <typename T>
 static hipError_t dmalloc(T **p, size_t bytes) {
-    hipError_t e = hipMallocAsync(reinterpret_cast<void **>(p), std::max<size_t>(bytes, 1), nullptr);
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
-    return e;
+    return hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(bytes, 1));
 }
 
 template <typename T>
@@ -434,10 +434,7 @@ static int upload(T **dptr, const std::vector<T> &v) {
 }
 
 static void dfree(void *p) {
-    if (p) {
-        (void)hipFreeAsync(p, nullptr);
-        (void)hipStreamSynchronize(nullptr);
-    }
+    if (p) (void)hipFree(p);
 }
 
 // nodes of one lane's backtrack tree: at most 2 * leaves - 1 <= 2 * n_kmers - 1
