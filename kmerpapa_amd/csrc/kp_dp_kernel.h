@@ -73,6 +73,17 @@ struct kp_dp_params {
 #endif
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
+#define KP_PIPE_CHUNKS 2  // pair-list chunks a thread loads one level ahead (8 pairs)
+
+// one low cell a thread will compute, prepared one level ahead (kp_dp_kernel level phase):
+// the cell, its pair list (first chunks loaded) and its single-pattern term as two float64
+// addends (kp_term), so no count or log is live across the barrier
+struct kp_lslot {
+    uint32_t cell;   // l | npairs << 16; 0xFFFFFFFF = no cell
+    uint32_t lpi;    // first 4-pair chunk of the cell's pair list (kp_plan.h lpairs)
+    uint4 pre[KP_PIPE_CHUNKS];
+    kp_term term;
+};
 
 // a workgroup-uniform 64-bit value (read by every lane from the same LDS word) into SGPRs
 __device__ inline uint64_t kp_rfl64(uint64_t v) {
@@ -265,8 +276,10 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     KP_STAMP(1);
 
     // ---- levels: low cells inside the block, level by level ----
-    // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
-    // the next level's descriptors are loaded while the current level computes
+    // one thread per cell: counts and the float64 logs once per cell for all NL lanes.
+    // Software-pipelined: everything a cell needs that does not depend on the DP values
+    // (descriptor, first pair-list chunks, counts, float64 logs) is prepared one level
+    // ahead, before the barrier, so a level's critical path is its LDS pair scan only.
     const bool high_zero = (P.H == 0);
     const int lmax = KP_SKIP(P, 2) ? -1 : P.lmax;
     const uint4 *desc = reinterpret_cast<const uint4 *>(P.T.ldesc);
@@ -274,92 +287,61 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     // cell's lanes over NL threads: the same work with a 1/NL-long dependent chain
     const int nthr = (int)blockDim.x;
     auto lane_split = [&](int cells) { return P.lanesplit && cells * NL <= nthr; };
-    uint4 cur[KP_IPT], nxt[KP_IPT];
-    {
-        const int beg = P.T.loff[0], cnt = P.T.loff[1] - beg;
-        if (lane_split(cnt)) {
-            if ((int)threadIdx.x / NL < cnt) cur[0] = desc[beg + (int)threadIdx.x / NL];
-        } else {
-#pragma unroll
-            for (int k = 0; k < KP_IPT; ++k) {
-                const int q = (int)threadIdx.x + k * nthr;
-                if (q < cnt) cur[k] = desc[beg + q];
-            }
-        }
-    }
-    for (int lam = 0; lam <= lmax; ++lam) {
+    // thread's cell of slot k at level lam, -1 if none (lane-split levels use slot 0 only)
+    auto cell_of = [&](int lam, int k) -> int {
         const int beg = P.T.loff[lam], cnt = P.T.loff[lam + 1] - beg;
-        if (lam < lmax) {
-            const int nbeg = P.T.loff[lam + 1], ncnt = P.T.loff[lam + 2] - nbeg;
-            if (lane_split(ncnt)) {
-                if ((int)threadIdx.x / NL < ncnt) nxt[0] = desc[nbeg + (int)threadIdx.x / NL];
-            } else {
-#pragma unroll
-                for (int k = 0; k < KP_IPT; ++k) {
-                    const int q = (int)threadIdx.x + k * nthr;
-                    if (q < ncnt) nxt[k] = desc[nbeg + q];
-                }
-            }
-        }
         if (lane_split(cnt)) {
             const int q = (int)threadIdx.x / NL;
-            const uint32_t j = threadIdx.x % NL;
-            if (q < cnt && !KP_SKIP(P, 8)) {
-                const uint32_t l = cur[0].x & 0xFFFFu;
-                const uint32_t info = cur[0].z;
-                const uint32_t npairs = cur[0].w & 0xFFu;
-                const uint4 *lp = P.T.lpairs + (cur[0].w >> 8);
-                uint4 pre[KP_PRE_CHUNKS];
-#pragma unroll
-                for (int c = 0; c < KP_PRE_CHUNKS; ++c)
-                    if (4u * c < npairs) pre[c] = lp[c];
-                kp_single_ctx sc;
-                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
-                sc.kmer = high_zero && lam == 0;
-                sc.c.mte = sc.c.ute = 0;
-                sc.logp = sc.log1mp = 0.0;
-                if (!sc.kmer) {
-                    const double pr = kp_rate(sc.c, alpha, beta);
-                    sc.logp = log(pr);
-                    sc.log1mp = log(1.0 - pr);
-                }
-                const double pj = G->pen[j];
-                kp_dp_cell_list<NL, 1>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, &pj, j);
-            }
-        } else
+            return (k == 0 && q < cnt) ? beg + q : -1;
+        }
+        const int q = (int)threadIdx.x + k * nthr;
+        return q < cnt ? beg + q : -1;
+    };
+    kp_lslot cur[KP_IPT], nxt[KP_IPT];
+    auto prep = [&](int lam, kp_lslot *sl) {
 #pragma unroll
         for (int k = 0; k < KP_IPT; ++k) {
-            const int q = (int)threadIdx.x + k * (int)blockDim.x;
-            if (q < cnt) {
-                const uint32_t l = cur[k].x & 0xFFFFu;
-                const uint32_t info = cur[k].z;
-                // the cell's split-pair list (plan tables, L2-resident): issued before the
-                // logs so the loads overlap them
-                const uint32_t npairs = cur[k].w & 0xFFu;
-                const uint4 *lp = P.T.lpairs + (cur[k].w >> 8);
-                uint4 pre[KP_PRE_CHUNKS];
+            const int e = (lam <= lmax) ? cell_of(lam, k) : -1;
+            sl[k].cell = 0xFFFFFFFFu;
+            if (e < 0) continue;
+            const uint4 d = desc[e];
+            const uint32_t l = d.x & 0xFFFFu, npairs = d.w & 0xFFu;
+            sl[k].cell = l | (npairs << 16);
+            sl[k].lpi = d.w >> 8;
+            const uint4 *lp = P.T.lpairs + sl[k].lpi;
 #pragma unroll
-                for (int c = 0; c < KP_PRE_CHUNKS; ++c)
-                    if (4u * c < npairs) pre[c] = lp[c];
-                // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
-                kp_single_ctx sc;
-                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
-                sc.kmer = high_zero && lam == 0;
-                sc.c.mte = sc.c.ute = 0;
-                sc.logp = sc.log1mp = 0.0;
-                if (!sc.kmer && !KP_SKIP(P, 4)) {
-                    const double pr = kp_rate(sc.c, alpha, beta);
-                    sc.logp = log(pr);
-                    sc.log1mp = log(1.0 - pr);
-                }
-                if (!KP_SKIP(P, 8)) {
-                    kp_dp_cell_list<NL, NL>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, pen);
-                } else {  // timing ablation: no split scan, keep the single term
+            for (int c = 0; c < KP_PIPE_CHUNKS; ++c)
+                if (4u * c < npairs) sl[k].pre[c] = lp[c];
+            // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
+            kp_cnt c;
+            kp_ptab_counts<CT>(g, lm, ptab, l, d.z, &c.mtr, &c.utr);
+            c.mte = c.ute = 0;
+            sl[k].term = kp_make_term(c, high_zero && lam == 0, alpha, beta, KP_SKIP(P, 4));
+        }
+    };
+    prep(0, cur);
+    for (int lam = 0; lam <= lmax; ++lam) {
+        const int cnt = P.T.loff[lam + 1] - P.T.loff[lam];
+        prep(lam + 1, nxt);  // reads no DP value: may run before this level's barrier
+        if (KP_SKIP(P, 8)) {  // timing ablation: no split scan, keep the single term
 #pragma unroll
-                    for (int j = 0; j < NL; ++j)
-                        st[l * NL + j] = (float)kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
-                }
+            for (int k = 0; k < KP_IPT; ++k)
+                if (cur[k].cell != 0xFFFFFFFFu && !lane_split(cnt))
+#pragma unroll
+                    for (int j = 0; j < NL; ++j) st[(cur[k].cell & 0xFFFFu) * NL + j] = kp_term_value(cur[k].term, pen[j]);
+        } else if (lane_split(cnt)) {
+            if (cur[0].cell != 0xFFFFFFFFu) {
+                const uint32_t j = threadIdx.x % NL;
+                const double pj = G->pen[j];
+                kp_dp_cell_term<NL, 1, KP_PIPE_CHUNKS>(cur[0].cell & 0xFFFFu, cur[0].cell >> 16, cur[0].pre,
+                                                       P.T.lpairs + cur[0].lpi, (kp_lds_f32 *)st, cur[0].term, &pj, j);
             }
+        } else {
+#pragma unroll
+            for (int k = 0; k < KP_IPT; ++k)
+                if (cur[k].cell != 0xFFFFFFFFu)
+                    kp_dp_cell_term<NL, NL, KP_PIPE_CHUNKS>(cur[k].cell & 0xFFFFu, cur[k].cell >> 16, cur[k].pre,
+                                                            P.T.lpairs + cur[k].lpi, (kp_lds_f32 *)st, cur[k].term, pen);
         }
         if (!KP_SKIP(P, 16)) __syncthreads();  // (ablation 16: timing without the level barrier)
         KP_STAMP(3 + lam);
