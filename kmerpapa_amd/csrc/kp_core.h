@@ -383,13 +383,22 @@ __host__ __device__ inline void kp_dp_cell_term(uint32_t l, uint32_t npairs, con
         for (int j = 0; j < W; ++j) row[j] = kp_term_value(t, pen[j]);
         return;
     }
+    // chunks PC .. PC+XC-1 are loaded first, so they land while the prefetched ones are scanned
+    constexpr int XC = 2;
+    uint4 extra[XC];
+#pragma unroll
+    for (int k = 0; k < XC; ++k)
+        if (4u * (PC + k) < npairs) extra[k] = lp[PC + k];
     float lmin[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) lmin[j] = row[j];
 #pragma unroll
     for (int k = 0; k < PC; ++k)
         if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
-    for (uint32_t k = PC; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+#pragma unroll
+    for (int k = 0; k < XC; ++k)
+        if (4u * (PC + k) < npairs) kp_chunk_minv<NL, W>(st, extra[k], j0, lmin);
+    for (uint32_t k = PC + XC; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
 #pragma unroll
     for (int j = 0; j < W; ++j) {
         float best = lmin[j];

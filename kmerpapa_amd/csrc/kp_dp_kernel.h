@@ -85,6 +85,12 @@ struct kp_lslot {
     kp_term term;
 };
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for
+// its outstanding global loads (__syncthreads would also drain those), so loads issued for
+// the next level (pair lists, descriptors) stay in flight across it.  Registers they fill
+// are waited for where they are used.
+__device__ inline void kp_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // a workgroup-uniform 64-bit value (read by every lane from the same LDS word) into SGPRs
 __device__ inline uint64_t kp_rfl64(uint64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
@@ -214,7 +220,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
 #pragma unroll
     for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
 
-    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | lm[t][16]
+    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | lm[t][16] | lof[lmax + 2]
     //      (count-table scratch aliases st, which the gather fills afterwards; every carve
     //       offset is a multiple of 16 bytes)
     const size_t st_bytes = (size_t)NL * Bpad * 4, scr_bytes = (size_t)P.pscratch_entries * 4 * sizeof(CT);
@@ -222,8 +228,9 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     CT *ptab = reinterpret_cast<CT *>(smem + (st_bytes > scr_bytes ? st_bytes : ((scr_bytes + 15) & ~(size_t)15)));
     kp_hpair *hp = reinterpret_cast<kp_hpair *>(ptab + (((size_t)P.ptab_entries * 2 + 3) & ~(size_t)3));
     uint8_t *lm = reinterpret_cast<uint8_t *>(hp + (g.kh * 7 + 1));
+    int32_t *lof = reinterpret_cast<int32_t *>(lm + ((g.t * 16 + 15) & ~15));  // level offsets [lmax + 2]
 #ifdef KP_STAMPS
-    unsigned long long *st_lds = reinterpret_cast<unsigned long long *>(lm + ((g.t * 16 + 15) & ~15));
+    unsigned long long *st_lds = reinterpret_cast<unsigned long long *>(lof + ((P.lmax + 2 + 3) & ~3));
     if (threadIdx.x < 32) st_lds[threadIdx.x] = 0;
 #endif
 
@@ -259,7 +266,8 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         hp[slot].code = (uint32_t)(((g.t + i) << 3) | rem);
     }
     for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 16u; e += blockDim.x) lm[e] = P.T.lowmask[e];
-    __syncthreads();  // lm is read by every thread below
+    for (int e = (int)threadIdx.x; e < P.lmax + 2; e += (int)blockDim.x) lof[e] = P.T.loff[e];
+    __syncthreads();  // lm and lof are read by every thread below
 
     // ---- separable count tables (train counts of the group fold), kp_core.h ----
     kp_build_count_table<CT>(g, K, h, fold, lm, reinterpret_cast<CT *>(smem),
@@ -287,9 +295,10 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     // cell's lanes over NL threads: the same work with a 1/NL-long dependent chain
     const int nthr = (int)blockDim.x;
     auto lane_split = [&](int cells) { return P.lanesplit && cells * NL <= nthr; };
+    const double pen_split = G->pen[threadIdx.x % NL];  // this thread's lane on lane-split levels
     // thread's cell of slot k at level lam, -1 if none (lane-split levels use slot 0 only)
     auto cell_of = [&](int lam, int k) -> int {
-        const int beg = P.T.loff[lam], cnt = P.T.loff[lam + 1] - beg;
+        const int beg = lof[lam], cnt = lof[lam + 1] - beg;
         if (lane_split(cnt)) {
             const int q = (int)threadIdx.x / NL;
             return (k == 0 && q < cnt) ? beg + q : -1;
@@ -297,32 +306,41 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         const int q = (int)threadIdx.x + k * nthr;
         return q < cnt ? beg + q : -1;
     };
-    kp_lslot cur[KP_IPT], nxt[KP_IPT];
+    // everything of level lam's cells that does not depend on DP values; the pair-list
+    // loads are issued last so nothing waits for them before the cells are computed
     auto prep = [&](int lam, kp_lslot *sl) {
+        uint4 d[KP_IPT];
 #pragma unroll
         for (int k = 0; k < KP_IPT; ++k) {
             const int e = (lam <= lmax) ? cell_of(lam, k) : -1;
             sl[k].cell = 0xFFFFFFFFu;
-            if (e < 0) continue;
-            const uint4 d = desc[e];
-            const uint32_t l = d.x & 0xFFFFu, npairs = d.w & 0xFFu;
-            sl[k].cell = l | (npairs << 16);
-            sl[k].lpi = d.w >> 8;
-            const uint4 *lp = P.T.lpairs + sl[k].lpi;
+            if (e >= 0) {
+                d[k] = desc[e];
+                sl[k].cell = (d[k].x & 0xFFFFu) | ((d[k].w & 0xFFu) << 16);
+                sl[k].lpi = d[k].w >> 8;
+            }
+        }
 #pragma unroll
-            for (int c = 0; c < KP_PIPE_CHUNKS; ++c)
-                if (4u * c < npairs) sl[k].pre[c] = lp[c];
+        for (int k = 0; k < KP_IPT; ++k) {
+            if (sl[k].cell == 0xFFFFFFFFu) continue;
             // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
             kp_cnt c;
-            kp_ptab_counts<CT>(g, lm, ptab, l, d.z, &c.mtr, &c.utr);
+            kp_ptab_counts<CT>(g, lm, ptab, sl[k].cell & 0xFFFFu, d[k].z, &c.mtr, &c.utr);
             c.mte = c.ute = 0;
             sl[k].term = kp_make_term(c, high_zero && lam == 0, alpha, beta, KP_SKIP(P, 4));
         }
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) {
+            if (sl[k].cell == 0xFFFFFFFFu) continue;
+            const uint4 *lp = P.T.lpairs + sl[k].lpi;
+#pragma unroll
+            for (int c = 0; c < KP_PIPE_CHUNKS; ++c)
+                if (4u * c < (sl[k].cell >> 16)) sl[k].pre[c] = lp[c];
+        }
     };
-    prep(0, cur);
-    for (int lam = 0; lam <= lmax; ++lam) {
-        const int cnt = P.T.loff[lam + 1] - P.T.loff[lam];
-        prep(lam + 1, nxt);  // reads no DP value: may run before this level's barrier
+    // one level from prepared slots, then the next level's preparation, then the barrier
+    auto level = [&](int lam, kp_lslot *cur, kp_lslot *nxt) {
+        const int cnt = lof[lam + 1] - lof[lam];
         if (KP_SKIP(P, 8)) {  // timing ablation: no split scan, keep the single term
 #pragma unroll
             for (int k = 0; k < KP_IPT; ++k)
@@ -331,10 +349,9 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                     for (int j = 0; j < NL; ++j) st[(cur[k].cell & 0xFFFFu) * NL + j] = kp_term_value(cur[k].term, pen[j]);
         } else if (lane_split(cnt)) {
             if (cur[0].cell != 0xFFFFFFFFu) {
-                const uint32_t j = threadIdx.x % NL;
-                const double pj = G->pen[j];
                 kp_dp_cell_term<NL, 1, KP_PIPE_CHUNKS>(cur[0].cell & 0xFFFFu, cur[0].cell >> 16, cur[0].pre,
-                                                       P.T.lpairs + cur[0].lpi, (kp_lds_f32 *)st, cur[0].term, &pj, j);
+                                                       P.T.lpairs + cur[0].lpi, (kp_lds_f32 *)st, cur[0].term,
+                                                       &pen_split, threadIdx.x % NL);
             }
         } else {
 #pragma unroll
@@ -343,10 +360,16 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
                     kp_dp_cell_term<NL, NL, KP_PIPE_CHUNKS>(cur[k].cell & 0xFFFFu, cur[k].cell >> 16, cur[k].pre,
                                                             P.T.lpairs + cur[k].lpi, (kp_lds_f32 *)st, cur[k].term, pen);
         }
-        if (!KP_SKIP(P, 16)) __syncthreads();  // (ablation 16: timing without the level barrier)
+        prep(lam + 1, nxt);  // reads no DP value: runs before this level's barrier
+        if (!KP_SKIP(P, 16)) kp_lds_barrier();  // (ablation 16: timing without the level barrier)
         KP_STAMP(3 + lam);
-#pragma unroll
-        for (int k = 0; k < KP_IPT; ++k) cur[k] = nxt[k];
+    };
+    // two slot sets used in turn (no copies between levels)
+    kp_lslot sa[KP_IPT], sb[KP_IPT];
+    prep(0, sa);
+    for (int lam = 0; lam <= lmax; lam += 2) {
+        level(lam, sa, sb);
+        if (lam + 1 <= lmax) level(lam + 1, sb, sa);
     }
 
     // ---- store the block's score rows ----
