@@ -339,80 +339,11 @@ __host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0,
 
 #define KP_PRE_CHUNKS 4  // pair-list chunks a thread loads ahead (16 pairs; longer lists load the rest on use)
 
-// A cell's single-pattern term for every penalty as two float64 addends, so that only two
-// doubles (not counts and logs) are carried to where the value is needed:
-//   k-mer cell (level 0):  s = a + pen,  a = -2 (xlogy(M, p) + xlog1py(U, -p))       (CV :15-20)
-//   wider cell:            s = (pen + a) + b,  a = (-2M) log p if M > 0 else -0.0,
-//                                              b = (-2U) log(1-p) if U > 0 else -0.0  (CV :63-70)
-// Adding -0.0 is the exact identity of IEEE addition (x + -0 = x for every x, -0 and NaN
-// included), so (pen + a) + b rounds exactly like the reference's conditional "s += ...".
-struct kp_term {
-    double a, b;
-    bool kmer;
-};
-
-__host__ __device__ inline kp_term kp_make_term(const kp_cnt &c, bool kmer, double alpha, double beta,
-                                                bool skip_logs = false) {
-    kp_term t;
-    t.kmer = kmer;
-    const double p = kp_rate(c, alpha, beta);
-    if (kmer) {
-        t.a = -2.0 * (kp_xlogy((double)c.mtr, p) + kp_xlog1py((double)c.utr, -p));
-        t.b = -0.0;
-        return t;
-    }
-    const double logp = skip_logs ? 0.0 : log(p), log1mp = skip_logs ? 0.0 : log(1.0 - p);
-    t.a = c.mtr > 0 ? (-2.0 * (double)c.mtr) * logp : -0.0;
-    t.b = c.utr > 0 ? (-2.0 * (double)c.utr) * log1mp : -0.0;
-    return t;
-}
-
-// the term's float64 value for penalty pen (the reference's s before its float32 store)
-__host__ __device__ inline double kp_term_s(const kp_term &t, double pen) {
-    return t.kmer ? t.a + pen : (pen + t.a) + t.b;
-}
-__host__ __device__ inline float kp_term_value(const kp_term &t, double pen) { return (float)kp_term_s(t, pen); }
-
-// kp_dp_cell_list with the single term as a kp_term (the sweep kernel's pipelined form)
-template <int NL, int W, int PC, typename SP>
-__host__ __device__ inline void kp_dp_cell_term(uint32_t l, uint32_t npairs, const uint4 *pre, const uint4 *lp, SP st,
-                                                const kp_term &t, const double *pen, uint32_t j0 = 0) {
-    SP row = st + l * NL + j0;
-    if (t.kmer) {  // level 0 (CV :145-151 / Fit :106-114)
-#pragma unroll
-        for (int j = 0; j < W; ++j) row[j] = kp_term_value(t, pen[j]);
-        return;
-    }
-    // chunks PC .. PC+XC-1 are loaded first, so they land while the prefetched ones are scanned
-    constexpr int XC = 2;
-    uint4 extra[XC];
-#pragma unroll
-    for (int k = 0; k < XC; ++k)
-        if (4u * (PC + k) < npairs) extra[k] = lp[PC + k];
-    float lmin[W];
-#pragma unroll
-    for (int j = 0; j < W; ++j) lmin[j] = row[j];
-#pragma unroll
-    for (int k = 0; k < PC; ++k)
-        if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
-#pragma unroll
-    for (int k = 0; k < XC; ++k)
-        if (4u * (PC + k) < npairs) kp_chunk_minv<NL, W>(st, extra[k], j0, lmin);
-    for (uint32_t k = PC + XC; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-        float best = lmin[j];
-        const double s = kp_term_s(t, pen[j]);
-        if (s < (double)best) best = (float)s;  // float64 compare against the float32 store (CV :71)
-        row[j] = best;
-    }
-}
-
 // The same cell from its flat split-pair list (the sweep kernel's form): npairs pairs in
 // 4-pair chunks, the first KP_PRE_CHUNKS already loaded into pre[] by the caller (so the
 // loads overlap the logs), the rest read from lp.  The wave runs as many chunks as its
 // longest list; shorter lists end in (B, B) pairs that read the +inf slot B.
-template <int NL, int W, int PC = KP_PRE_CHUNKS, typename SP>
+template <int NL, int W, typename SP>
 __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, const uint4 *pre, const uint4 *lp, SP st,
                                                 const kp_single_ctx &sc, double alpha, double beta,
                                                 const double *pen, uint32_t j0 = 0) {
@@ -426,9 +357,9 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
 #pragma unroll
     for (int j = 0; j < W; ++j) lmin[j] = row[j];
 #pragma unroll
-    for (int k = 0; k < PC; ++k)
+    for (int k = 0; k < KP_PRE_CHUNKS; ++k)
         if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
-    for (uint32_t k = PC; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+    for (uint32_t k = KP_PRE_CHUNKS; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
     kp_cell_store<W>(row, lmin, sc, pen);
 }
 

@@ -73,23 +73,6 @@ struct kp_dp_params {
 #endif
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
-#define KP_PIPE_CHUNKS 2  // pair-list chunks a thread loads one level ahead (8 pairs)
-
-// one low cell a thread will compute, prepared one level ahead (kp_dp_kernel level phase):
-// the cell, its pair list (first chunks loaded) and its single-pattern term as two float64
-// addends (kp_term), so no count or log is live across the barrier
-struct kp_lslot {
-    uint32_t cell;   // l | npairs << 16; 0xFFFFFFFF = no cell
-    uint32_t lpi;    // first 4-pair chunk of the cell's pair list (kp_plan.h lpairs)
-    uint4 pre[KP_PIPE_CHUNKS];
-    kp_term term;
-};
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for
-// its outstanding global loads (__syncthreads would also drain those), so loads issued for
-// the next level (pair lists, descriptors) stay in flight across it.  Registers they fill
-// are waited for where they are used.
-__device__ inline void kp_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // a workgroup-uniform 64-bit value (read by every lane from the same LDS word) into SGPRs
 __device__ inline uint64_t kp_rfl64(uint64_t v) {
@@ -220,7 +203,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
 #pragma unroll
     for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
 
-    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | lm[t][16] | lof[lmax + 2]
+    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | lm[t][16]
     //      (count-table scratch aliases st, which the gather fills afterwards; every carve
     //       offset is a multiple of 16 bytes)
     const size_t st_bytes = (size_t)NL * Bpad * 4, scr_bytes = (size_t)P.pscratch_entries * 4 * sizeof(CT);
@@ -228,9 +211,8 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     CT *ptab = reinterpret_cast<CT *>(smem + (st_bytes > scr_bytes ? st_bytes : ((scr_bytes + 15) & ~(size_t)15)));
     kp_hpair *hp = reinterpret_cast<kp_hpair *>(ptab + (((size_t)P.ptab_entries * 2 + 3) & ~(size_t)3));
     uint8_t *lm = reinterpret_cast<uint8_t *>(hp + (g.kh * 7 + 1));
-    int32_t *lof = reinterpret_cast<int32_t *>(lm + ((g.t * 16 + 15) & ~15));  // level offsets [lmax + 2]
 #ifdef KP_STAMPS
-    unsigned long long *st_lds = reinterpret_cast<unsigned long long *>(lof + ((P.lmax + 2 + 3) & ~3));
+    unsigned long long *st_lds = reinterpret_cast<unsigned long long *>(lm + ((g.t * 16 + 15) & ~15));
     if (threadIdx.x < 32) st_lds[threadIdx.x] = 0;
 #endif
 
@@ -266,8 +248,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
         hp[slot].code = (uint32_t)(((g.t + i) << 3) | rem);
     }
     for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 16u; e += blockDim.x) lm[e] = P.T.lowmask[e];
-    for (int e = (int)threadIdx.x; e < P.lmax + 2; e += (int)blockDim.x) lof[e] = P.T.loff[e];
-    __syncthreads();  // lm and lof are read by every thread below
+    __syncthreads();  // lm is read by every thread below
 
     // ---- separable count tables (train counts of the group fold), kp_core.h ----
     kp_build_count_table<CT>(g, K, h, fold, lm, reinterpret_cast<CT *>(smem),
@@ -284,10 +265,8 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     KP_STAMP(1);
 
     // ---- levels: low cells inside the block, level by level ----
-    // one thread per cell: counts and the float64 logs once per cell for all NL lanes.
-    // Software-pipelined: everything a cell needs that does not depend on the DP values
-    // (descriptor, first pair-list chunks, counts, float64 logs) is prepared one level
-    // ahead, before the barrier, so a level's critical path is its LDS pair scan only.
+    // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
+    // the next level's descriptors are loaded while the current level computes
     const bool high_zero = (P.H == 0);
     const int lmax = KP_SKIP(P, 2) ? -1 : P.lmax;
     const uint4 *desc = reinterpret_cast<const uint4 *>(P.T.ldesc);
@@ -295,81 +274,97 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     // cell's lanes over NL threads: the same work with a 1/NL-long dependent chain
     const int nthr = (int)blockDim.x;
     auto lane_split = [&](int cells) { return P.lanesplit && cells * NL <= nthr; };
-    const double pen_split = G->pen[threadIdx.x % NL];  // this thread's lane on lane-split levels
-    // thread's cell of slot k at level lam, -1 if none (lane-split levels use slot 0 only)
-    auto cell_of = [&](int lam, int k) -> int {
-        const int beg = lof[lam], cnt = lof[lam + 1] - beg;
+    uint4 cur[KP_IPT], nxt[KP_IPT];
+    {
+        const int beg = P.T.loff[0], cnt = P.T.loff[1] - beg;
         if (lane_split(cnt)) {
-            const int q = (int)threadIdx.x / NL;
-            return (k == 0 && q < cnt) ? beg + q : -1;
-        }
-        const int q = (int)threadIdx.x + k * nthr;
-        return q < cnt ? beg + q : -1;
-    };
-    // everything of level lam's cells that does not depend on DP values; the pair-list
-    // loads are issued last so nothing waits for them before the cells are computed
-    auto prep = [&](int lam, kp_lslot *sl) {
-        uint4 d[KP_IPT];
-#pragma unroll
-        for (int k = 0; k < KP_IPT; ++k) {
-            const int e = (lam <= lmax) ? cell_of(lam, k) : -1;
-            sl[k].cell = 0xFFFFFFFFu;
-            if (e >= 0) {
-                d[k] = desc[e];
-                sl[k].cell = (d[k].x & 0xFFFFu) | ((d[k].w & 0xFFu) << 16);
-                sl[k].lpi = d[k].w >> 8;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < KP_IPT; ++k) {
-            if (sl[k].cell == 0xFFFFFFFFu) continue;
-            // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
-            kp_cnt c;
-            kp_ptab_counts<CT>(g, lm, ptab, sl[k].cell & 0xFFFFu, d[k].z, &c.mtr, &c.utr);
-            c.mte = c.ute = 0;
-            sl[k].term = kp_make_term(c, high_zero && lam == 0, alpha, beta, KP_SKIP(P, 4));
-        }
-#pragma unroll
-        for (int k = 0; k < KP_IPT; ++k) {
-            if (sl[k].cell == 0xFFFFFFFFu) continue;
-            const uint4 *lp = P.T.lpairs + sl[k].lpi;
-#pragma unroll
-            for (int c = 0; c < KP_PIPE_CHUNKS; ++c)
-                if (4u * c < (sl[k].cell >> 16)) sl[k].pre[c] = lp[c];
-        }
-    };
-    // one level from prepared slots, then the next level's preparation, then the barrier
-    auto level = [&](int lam, kp_lslot *cur, kp_lslot *nxt) {
-        const int cnt = lof[lam + 1] - lof[lam];
-        if (KP_SKIP(P, 8)) {  // timing ablation: no split scan, keep the single term
-#pragma unroll
-            for (int k = 0; k < KP_IPT; ++k)
-                if (cur[k].cell != 0xFFFFFFFFu && !lane_split(cnt))
-#pragma unroll
-                    for (int j = 0; j < NL; ++j) st[(cur[k].cell & 0xFFFFu) * NL + j] = kp_term_value(cur[k].term, pen[j]);
-        } else if (lane_split(cnt)) {
-            if (cur[0].cell != 0xFFFFFFFFu) {
-                kp_dp_cell_term<NL, 1, KP_PIPE_CHUNKS>(cur[0].cell & 0xFFFFu, cur[0].cell >> 16, cur[0].pre,
-                                                       P.T.lpairs + cur[0].lpi, (kp_lds_f32 *)st, cur[0].term,
-                                                       &pen_split, threadIdx.x % NL);
-            }
+            if ((int)threadIdx.x / NL < cnt) cur[0] = desc[beg + (int)threadIdx.x / NL];
         } else {
 #pragma unroll
-            for (int k = 0; k < KP_IPT; ++k)
-                if (cur[k].cell != 0xFFFFFFFFu)
-                    kp_dp_cell_term<NL, NL, KP_PIPE_CHUNKS>(cur[k].cell & 0xFFFFu, cur[k].cell >> 16, cur[k].pre,
-                                                            P.T.lpairs + cur[k].lpi, (kp_lds_f32 *)st, cur[k].term, pen);
+            for (int k = 0; k < KP_IPT; ++k) {
+                const int q = (int)threadIdx.x + k * nthr;
+                if (q < cnt) cur[k] = desc[beg + q];
+            }
         }
-        prep(lam + 1, nxt);  // reads no DP value: runs before this level's barrier
-        if (!KP_SKIP(P, 16)) kp_lds_barrier();  // (ablation 16: timing without the level barrier)
+    }
+    for (int lam = 0; lam <= lmax; ++lam) {
+        const int beg = P.T.loff[lam], cnt = P.T.loff[lam + 1] - beg;
+        if (lam < lmax) {
+            const int nbeg = P.T.loff[lam + 1], ncnt = P.T.loff[lam + 2] - nbeg;
+            if (lane_split(ncnt)) {
+                if ((int)threadIdx.x / NL < ncnt) nxt[0] = desc[nbeg + (int)threadIdx.x / NL];
+            } else {
+#pragma unroll
+                for (int k = 0; k < KP_IPT; ++k) {
+                    const int q = (int)threadIdx.x + k * nthr;
+                    if (q < ncnt) nxt[k] = desc[nbeg + q];
+                }
+            }
+        }
+        if (lane_split(cnt)) {
+            const int q = (int)threadIdx.x / NL;
+            const uint32_t j = threadIdx.x % NL;
+            if (q < cnt && !KP_SKIP(P, 8)) {
+                const uint32_t l = cur[0].x & 0xFFFFu;
+                const uint32_t info = cur[0].z;
+                const uint32_t npairs = cur[0].w & 0xFFu;
+                const uint4 *lp = P.T.lpairs + (cur[0].w >> 8);
+                uint4 pre[KP_PRE_CHUNKS];
+#pragma unroll
+                for (int c = 0; c < KP_PRE_CHUNKS; ++c)
+                    if (4u * c < npairs) pre[c] = lp[c];
+                kp_single_ctx sc;
+                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
+                sc.kmer = high_zero && lam == 0;
+                sc.c.mte = sc.c.ute = 0;
+                sc.logp = sc.log1mp = 0.0;
+                if (!sc.kmer) {
+                    const double pr = kp_rate(sc.c, alpha, beta);
+                    sc.logp = log(pr);
+                    sc.log1mp = log(1.0 - pr);
+                }
+                const double pj = G->pen[j];
+                kp_dp_cell_list<NL, 1>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, &pj, j);
+            }
+        } else
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) {
+            const int q = (int)threadIdx.x + k * (int)blockDim.x;
+            if (q < cnt) {
+                const uint32_t l = cur[k].x & 0xFFFFu;
+                const uint32_t info = cur[k].z;
+                // the cell's split-pair list (plan tables, L2-resident): issued before the
+                // logs so the loads overlap them
+                const uint32_t npairs = cur[k].w & 0xFFu;
+                const uint4 *lp = P.T.lpairs + (cur[k].w >> 8);
+                uint4 pre[KP_PRE_CHUNKS];
+#pragma unroll
+                for (int c = 0; c < KP_PRE_CHUNKS; ++c)
+                    if (4u * c < npairs) pre[c] = lp[c];
+                // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
+                kp_single_ctx sc;
+                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
+                sc.kmer = high_zero && lam == 0;
+                sc.c.mte = sc.c.ute = 0;
+                sc.logp = sc.log1mp = 0.0;
+                if (!sc.kmer && !KP_SKIP(P, 4)) {
+                    const double pr = kp_rate(sc.c, alpha, beta);
+                    sc.logp = log(pr);
+                    sc.log1mp = log(1.0 - pr);
+                }
+                if (!KP_SKIP(P, 8)) {
+                    kp_dp_cell_list<NL, NL>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, pen);
+                } else {  // timing ablation: no split scan, keep the single term
+#pragma unroll
+                    for (int j = 0; j < NL; ++j)
+                        st[l * NL + j] = (float)kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
+                }
+            }
+        }
+        if (!KP_SKIP(P, 16)) __syncthreads();  // (ablation 16: timing without the level barrier)
         KP_STAMP(3 + lam);
-    };
-    // two slot sets used in turn (no copies between levels)
-    kp_lslot sa[KP_IPT], sb[KP_IPT];
-    prep(0, sa);
-    for (int lam = 0; lam <= lmax; lam += 2) {
-        level(lam, sa, sb);
-        if (lam + 1 <= lmax) level(lam + 1, sb, sa);
+#pragma unroll
+        for (int k = 0; k < KP_IPT; ++k) cur[k] = nxt[k];
     }
 
     // ---- store the block's score rows ----

@@ -607,7 +607,7 @@ static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
     const size_t scratch = (((size_t)hp.pscratch_entries * 4 * ct_bytes) + 15) & ~(size_t)15;  // 2 build buffers
     const size_t ptab = ((((size_t)hp.ptab_entries * 2 + 3) & ~(size_t)3)) * ct_bytes;
     return std::max(st, scratch) + ptab + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) +
-           (((size_t)g.t * 16 + 15) & ~(size_t)15) + (((size_t)hp.lmax + 2 + 3) & ~(size_t)3) * 4 + 16
+           (((size_t)g.t * 16 + 15) & ~(size_t)15) + 16
 #ifdef KP_STAMPS
            + 32 * sizeof(unsigned long long)
 #endif
