@@ -66,3 +66,22 @@ def test_oracle_grid5_roots():
         r = O.cv_pass(g["gen_pat"], kmers, F["M5"], F["U5"], ps["alpha"], ps["betas"], ps["penalty"], 32)
         assert bits_equal(r["root_train"], np.array(ps["root_train"], np.float32))
         assert bits_equal(r["root_test"], np.array(ps["root_test"], np.float32))
+
+
+def test_oracle_cv7_roots_vs_reference():
+    """Config 3 (7-mer test data, 34,171,875 cells, 5 folds) through the oracle: per-fold
+    root train/test values of two of the grid's nine (alpha, c) points equal the reference's
+    own (tests/golden/cv7.json, one reference process per point, make_golden.py cv7p_*).
+    The oracle runs each level over the host's cores (same values as one thread)."""
+    import os
+    g = golden_json("cv7.json")
+    if g is None:
+        pytest.skip("cv7 golden not generated")
+    F = golden_npz("folds.npz")
+    kmers = [str(x) for x in F["kmers7"]]
+    threads = max(1, min(8, len(os.sched_getaffinity(0))))
+    for ps in (g["passes"][0], g["passes"][-1]):
+        r = O.cv_pass(g["gen_pat"], kmers, F["M7"], F["U7"], ps["alpha"], ps["betas"], ps["penalty"], 32,
+                      threads=threads)
+        assert bits_equal(r["root_train"], np.array(ps["root_train"], np.float32))
+        assert bits_equal(r["root_test"], np.array(ps["root_test"], np.float32))
