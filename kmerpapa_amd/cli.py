@@ -8,7 +8,10 @@ they are accepted by the parser and rejected with a message.  ``--score all_kmer
 rate per k-mer, no lattice DP) runs on the host (algorithms/all_kmers_CV.py).
 """
 import argparse
+import json
+import os
 import sys
+import time
 from math import log
 
 from . import __version__
@@ -80,8 +83,32 @@ def _out_of_scope(args):
     return None
 
 
+class _Phases:
+    """Wall-clock per phase of one run.  With $KMERPAPA_METRICS set to a file path, one JSON
+    line is appended there at the end (no reference counterpart; SURVEY.md 5 metrics)."""
+
+    def __init__(self):
+        self.t0 = self.last = time.perf_counter()
+        self.phases = {}
+
+    def mark(self, name):
+        now = time.perf_counter()
+        self.phases[name] = self.phases.get(name, 0.0) + (now - self.last)
+        self.last = now
+
+    def write(self, **extra):
+        path = os.environ.get("KMERPAPA_METRICS")
+        if not path:
+            return
+        rec = dict(extra, phases_s={k: round(v, 4) for k, v in self.phases.items()},
+                   total_s=round(time.perf_counter() - self.t0, 4))
+        with open(path, "a") as fh:
+            fh.write(json.dumps(rec) + "\n")
+
+
 def main(args=None):
     """Run the program (cli.py:118-318).  Returns an exit code."""
+    clock = _Phases()
     parser = get_parser()
     args = parser.parse_args(args=args)
     if args.version:
@@ -102,6 +129,7 @@ def main(args=None):
         print(e, file=sys.stderr)
         print("=" * 80, file=sys.stderr)
         return 0
+    clock.mark("read_input")
     verbose = args.verbosity > 0
     if verbose:
         print(f"Input data read. {n_mut} positive k-mers and {n_unmut} negative k-mers", file=sys.stderr)
@@ -131,6 +159,7 @@ def main(args=None):
         print(f"General pattern: {gen_pat}", file=sys.stderr)
     if args.CVfile is not None:
         print("k alpha P LL_test", file=args.CVfile)
+    clock.mark("pattern_and_zero_fill")
 
     best_alpha = best_penalty = best_k = None
     ks = range(len(gen_pat), 1, -2) if args.test_smaller_k else [len(gen_pat)]
@@ -160,7 +189,9 @@ def main(args=None):
                   f"best_test_LL={best_score}", file=sys.stderr)
     if args.CVfile is not None:
         args.CVfile.close()
+    clock.mark("cross_validation")
     if args.CV_only:
+        clock.write(gen_pat=gen_pat, cv_only=True)
         return 0
 
     if best_alpha is None:
@@ -186,6 +217,7 @@ def main(args=None):
         best_score, M, U, names = bottum_up_array_w_numba.pattern_partition_bottom_up(
             gen_pat, contextD, best_alpha, best_beta, best_penalty, args, n_mut, n_unmut)
         counts = contextD.pattern_counts(names)  # get_M_U per pattern (cli.py:287)
+    clock.mark("final_fit")
     # partition sanity checks of the reference (cli.py:289-292)
     assert M == n_mut
     assert U == n_unmut
@@ -209,4 +241,6 @@ def main(args=None):
             out.write("".join(f"{context} {ns} {nm} {float(nm) / (nm + ns)}{tail}" for context, nm, ns in zip(*rows)))
         else:
             print(pat, Up, Mp, p, file=out)
+    clock.mark("output")
+    clock.write(gen_pat=gen_pat, patterns=len(names), best_alpha=best_alpha, best_penalty=best_penalty)
     return 0

@@ -385,3 +385,18 @@ def test_error_paths(eng):
         eng.Plan(dev, "NXN", 0)  # not an IUPAC code
     with pytest.raises(eng.KPError, match="too many blocks"):
         eng.Plan(dev, "NNNNNNNNNNNN", 0)  # 15^12 cells: more blocks than 32-bit ids
+
+
+def test_cli_metrics_line(eng, tmp_path, monkeypatch):
+    """$KMERPAPA_METRICS: one JSON line per run with the wall-clock of every phase."""
+    import json
+    from kmerpapa_amd import cli
+    pos, bg = write_count_files(5, str(tmp_path))
+    metrics = tmp_path / "m.jsonl"
+    monkeypatch.setenv("KMERPAPA_METRICS", str(metrics))
+    assert cli.main(["-p", pos, "-b", bg, "-c", "3", "5", "-a", "0.5", "1", "--nfolds", "3", "--seed", "2",
+                     "-o", str(tmp_path / "o.txt")]) == 0
+    rec = json.loads(metrics.read_text().splitlines()[-1])
+    assert set(rec["phases_s"]) == {"read_input", "pattern_and_zero_fill", "cross_validation", "final_fit", "output"}
+    assert rec["gen_pat"] == "NNMNN" and rec["patterns"] > 1
+    assert abs(sum(rec["phases_s"].values()) - rec["total_s"]) < 0.05

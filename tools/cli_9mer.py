@@ -22,9 +22,13 @@ with open(os.path.join(out, "bg.txt"), "w") as f:
 cmd = [sys.executable, "-m", "kmerpapa_amd", "-p", os.path.join(out, "pos.txt"), "-b", os.path.join(out, "bg.txt"),
        "-c", "3", "4", "5", "6", "7", "-a", "0.5", "1", "2", "5", "10", "--nfolds", "5", "--seed", "1",
        "-o", os.path.join(out, "partition.txt"), "-f", os.path.join(out, "cv.txt")]
+metrics = os.path.join(out, "metrics.jsonl")
+if os.path.exists(metrics):
+    os.remove(metrics)
 t0 = time.time()
-r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True)
+r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, env=dict(os.environ, KMERPAPA_METRICS=metrics))
 wall = time.time() - t0
+phases = json.loads(open(metrics).read().splitlines()[-1]) if os.path.exists(metrics) else None
 lines = open(os.path.join(out, "partition.txt")).read().splitlines() if r.returncode == 0 else []
 print(json.dumps({"cmd": " ".join(cmd[1:]), "rc": r.returncode, "wall_s": wall, "patterns": max(0, len(lines) - 1),
-                  "stderr_tail": r.stderr[-1500:]}))
+                  "in_process": phases, "stderr_tail": r.stderr[-600:]}))
