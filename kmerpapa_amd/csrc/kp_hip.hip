@@ -796,8 +796,12 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
             while (j < dg.size() && dg[j].nl == dg[i].nl) ++j;
             kp_dp_params Q = P;
             Q.groups = p->d_groups + i;
-            int rc = launch_dp_nl<CT>(dg[i].nl, c, Q, (unsigned)nb, (unsigned)(j - i), threads,
-                                      dp_lds_bytes(hp, dg[i].nl, sizeof(CT)));
+            size_t lds = dp_lds_bytes(hp, dg[i].nl, sizeof(CT));
+#ifdef KP_ABLATION
+            // ablation build only: extra LDS per workgroup to force lower occupancy
+            if (getenv("KP_LDS_PAD")) lds += (size_t)atol(getenv("KP_LDS_PAD"));
+#endif
+            int rc = launch_dp_nl<CT>(dg[i].nl, c, Q, (unsigned)nb, (unsigned)(j - i), threads, lds);
             if (rc) return rc;
             ++launches;
             i = j;

@@ -185,12 +185,24 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
             sigs[l] = sig;
             npairs[l] = np;
         }
+        // KP_LOW_ORDER=1 (experiment): inside a pair-count class, cells with the same digits
+        // at every ambiguous low position next to each other, so a wave's split children sit
+        // at the same offsets from consecutive-ish cells (fewer LDS bank conflicts)
+        const char *lo = getenv("KP_LOW_ORDER");
+        const bool bydig = lo && atoi(lo) == 1;
+        std::vector<uint32_t> amb(B, 0);  // digits at ambiguous positions, nucleotides zeroed
+        for (uint32_t l = 0; l < B; ++l)
+            for (int i = 0; i < t; ++i) {
+                const uint32_t d = kp_low_digit(P.lowinfo[l], i);
+                if (P.tabs[i].np[d]) amb[l] |= d << (4 * i);
+            }
         std::vector<uint32_t> idx(B);
         for (uint32_t l = 0; l < B; ++l) idx[l] = l;
         std::sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
             if (llev[a] != llev[b]) return llev[a] < llev[b];
             if (npairs[a] != npairs[b]) return npairs[a] < npairs[b];
             if (sigs[a] != sigs[b]) return sigs[a] < sigs[b];
+            if (bydig && amb[a] != amb[b]) return amb[a] < amb[b];
             return a < b;
         });
         for (uint32_t q = 0; q < B; ++q) P.lorder[q] = (uint16_t)idx[q];

@@ -1,17 +1,31 @@
-"""Scratch: time 9-mer passes under env variants (KP_DEBUG_SKIP ablates phases -> wrong
-results, timing only; KP_LANES_PER_WG changes lanes per workgroup)."""
-import json, os, subprocess, sys
-variants = [v.split(",") for v in sys.argv[1:]] or [["KP_DEBUG_SKIP=0"]]
-for var in variants:
-    env = dict(os.environ)
-    for kv in var:
-        k, v = kv.split("=")
-        env[k] = v
-    out = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline"],
-                         env=env, capture_output=True, text=True)
-    try:
-        d = json.loads(out.stdout.strip().splitlines()[-1])
-        print(var, "dp_ms %.1f bt_ms %.1f step_ms %.1f" % (d["dp_kernel_ms_per_step"], d["backtrack_ms_per_step"],
-                                                           d["ms_per_step"]), flush=True)
-    except Exception:
-        print(var, "failed", out.stderr[-800:], flush=True)
+"""Phase ablations of the 9-mer sweep (tool): kernel time of one 5-lane pass with phases
+skipped.  Needs the timing-ablation build (make -C kmerpapa_amd/csrc ablation) and
+KMERPAPA_LIB=kmerpapa_amd/libkmerpapa_hip_ablation.so; every ablated pass returns
+KP_E_STATE (its numbers are invalid) after recording its timings.
+usage: python tools/ablate.py SKIP [SKIP ...]   (KP_DEBUG_SKIP bit sets, 0 = full pass)
+  1 = no gather, 2 = no level phase, 4 = no float64 logs, 8 = no low split scan,
+  16 = no level barriers"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from kmerpapa_amd import engine  # noqa: E402
+
+prep = bench.prepare("NNNNMNNNN")
+plan = engine.get_plan(0, "NNNNMNNNN")
+plan.set_counts(prep["Mk"], prep["Uk"])
+plan.reserve(5)
+g = prep["groups"][0]
+for skip in sys.argv[1:] or ["0"]:
+    os.environ["KP_DEBUG_SKIP"] = skip
+    ms = []
+    for rep in range(3):
+        try:
+            plan.run([g])
+        except engine.KPError as e:
+            if e.code != -4 or skip == "0":  # KP_E_STATE: an ablated pass
+                raise
+        ms.append(plan.stats()["dp_ms"])
+    print(json.dumps({"KP_DEBUG_SKIP": int(skip), "dp_ms": [round(x, 2) for x in ms]}), flush=True)
