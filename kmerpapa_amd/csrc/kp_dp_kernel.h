@@ -174,8 +174,16 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
     }
 }
 
+// Groups of 1-3 lanes (penalties split off their (alpha, fold) group, e.g. by the
+// multi-GPU lane split) are latency-bound and their LDS fits 3 workgroups per CU: ask for
+// KP_SMALL_WAVES waves per SIMD (6: <= 80 VGPRs, 3 workgroups of 512 threads per CU;
+// 1-lane pass 188 -> 157 ms) and gather 2 items per thread instead of 4
+#ifndef KP_SMALL_WAVES
+#define KP_SMALL_WAVES 6
+#endif
 template <typename CT, int NL>
-__global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P) {
+__global__ void __launch_bounds__(KP_DP_MAX_THREADS) __attribute__((amdgpu_waves_per_eu(NL <= 3 ? KP_SMALL_WAVES : 1)))
+kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const kp_geom &g = P.g;
 #ifdef KP_STAMPS
@@ -260,7 +268,7 @@ __global__ void __launch_bounds__(KP_DP_MAX_THREADS) kp_dp_kernel(kp_dp_params P
     // ---- gather: high-position splits, as whole child-block rows (value only) ----
     // four float4 items per thread at a time, two pairs per step: 16 row loads in flight
     // per thread even when the block has few pairs (measured best of 1-4 items x 1-4 pairs)
-    kp_gather_items<NL, 4, 2>(P, hp, np, nnt, lane0, st);
+    kp_gather_items<NL, (NL <= 3 ? 2 : 4), 2>(P, hp, np, nnt, lane0, st);
     __syncthreads();
     KP_STAMP(1);
 
