@@ -1,0 +1,46 @@
+"""bench.py's host-side helpers (no GPU): the synthetic count table is the CLI's sorted
+array table, the 8-rank CV shares cover every (alpha, fold, penalty) lane exactly once in
+lane order, and passes never exceed one group's lanes."""
+import numpy as np
+
+import bench
+from kmerpapa_amd import engine
+from kmerpapa_amd.io_utils import KmerCounts
+
+
+def test_kmer_table_is_sorted_and_complete():
+    kmers, M, U = bench.synthetic_counts("NMN", seed=3)
+    t = bench.kmer_table(kmers, M, U)
+    assert isinstance(t, KmerCounts)
+    assert list(t) == sorted(kmers)
+    for k, m, u in zip(kmers, M, U):
+        assert t[k] == (int(m), int(u))
+
+
+def _prep(nfolds=5, alphas=(0.5, 1.0, 2.0, 5.0, 10.0), pens=(3.0, 4.0, 5.0, 6.0, 7.0)):
+    groups = [(f, a, 0.1 * (f + 1) * a, list(pens)) for a in alphas for f in range(nfolds)]
+    return {"groups": groups}
+
+
+def test_cv_shares_cover_every_lane_once():
+    prep = _prep()
+    want = [(g[0], g[1], c) for g in prep["groups"] for c in g[3]]
+    for world in (1, 2, 3, 8):
+        cap = engine.pass_cap(prep["groups"], 9)
+        shares = bench.cv_shares(prep, world, cap)
+        got = [(g[0], g[1], c) for passes in shares for p in passes for g in p for c in g[3]]
+        assert got == want
+        assert all(sum(len(g[3]) for g in p) <= cap for passes in shares for p in passes)
+        lanes = [sum(len(g[3]) for p in passes for g in p) for passes in shares]
+        assert max(lanes) - min(lanes) <= 1
+
+
+def test_pass_cap_is_largest_group_if_it_fits():
+    groups = [(0, 1.0, 1.0, [1.0] * 5), (1, 1.0, 1.0, [1.0] * 3)]
+    assert engine.pass_cap(groups, 9) == 5
+    assert engine.pass_cap(groups, 4) == 4
+    assert engine.pass_cap([], 9) == 1
+
+
+def test_host_cores_positive():
+    assert bench.host_cores() >= 1

@@ -11,6 +11,8 @@ import bench  # noqa: E402
 from kmerpapa_amd import engine  # noqa: E402
 
 comps = [[5], [1], [2], [3], [4], [5, 1], [4, 4], [3, 3, 2], [5, 3]]
+if len(sys.argv) > 1:  # e.g. "5 3,2": compositions as comma lists
+    comps = [[int(x) for x in a.split(",")] for a in sys.argv[1:]]
 prep = bench.prepare("NNNNMNNNN")
 plan = engine.get_plan(0, "NNNNMNNNN")
 plan.set_counts(prep["Mk"], prep["Uk"])
