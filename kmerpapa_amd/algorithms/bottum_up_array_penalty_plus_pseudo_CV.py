@@ -149,7 +149,8 @@ def _distributed_runner():
         if dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             import os
             from ..shard import sharded_run_groups, torch_all_gather
-            local = int(os.environ.get("LOCAL_RANK", "0"))
+            # one GPU per rank; more ranks than GPUs (a rehearsal) share them round-robin
+            local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, engine.device_count())
             return sharded_run_groups(engine.run_groups, dist.get_rank(), dist.get_world_size(),
                                       torch_all_gather(), devices=[local]), [local]
     except ImportError:
