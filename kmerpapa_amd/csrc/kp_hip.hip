@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <string>
@@ -380,6 +381,7 @@ struct kp_plan {
     int ct_bytes = 0;
     // lanes
     float *d_S = nullptr;
+    bool S_pool = false;  // d_S came from the device's stream-ordered pool (see alloc_scores)
     uint64_t lanes_cap = 0;
     kp_node *d_nodes = nullptr;
     uint32_t node_cap = 0;  // nodes per lane
@@ -397,6 +399,8 @@ struct kp_plan {
     std::vector<uint32_t> last_lanegrp;
     kp_pass_stats stats{};
 };
+
+static void free_scores(kp_plan *p);  // the score rows (pool or hipMalloc), defined below
 
 static kp_dev_tables tables_of(const kp_plan *p) {
     kp_dev_tables T;
@@ -513,8 +517,9 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
 void kp_plan_destroy(kp_plan *p) {
     if (!p) return;
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
+    free_scores(p);
     void *bufs[] = {p->d_tabs,    p->d_lowinfo, p->d_loff,   p->d_klofs,   p->d_kllist, p->d_hlist, p->d_ldesc,
-                    p->d_hdig,    p->d_lowmask, p->d_lpairs, p->d_K,      p->d_S,      p->d_nodes, p->d_groups,
+                    p->d_hdig,    p->d_lowmask, p->d_lpairs, p->d_K,      p->d_nodes, p->d_groups,
                     p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
                     p->d_leaves};
     for (void *b : bufs) dfree(b);
@@ -657,11 +662,79 @@ static int lanes_per_wg_default() {
 // before any read.  Freeing and re-allocating a large buffer is slow on this platform
 // (the driver wipes freed memory before handing it out again: ~4 s for 100-150 GB,
 // tools/alloc_probe.hip), so callers reserve the largest pass up front (kp_reserve_lanes).
+// ---- the score rows: the one very large allocation ----
+// A hipMalloc of HBM that was used before waits for the driver's wipe (~30 ms per GB).
+// The device's stream-ordered pool does not, but re-serving a freed pool block for a larger
+// request returned corrupt memory at >= 140 GB (tools/async_check.hip).  So: the FIRST score
+// buffer of a process on a device comes from the pool (nothing was ever freed there), is
+// written with a pattern and read back before use, and every later one (after a free, or
+// if the check fails) comes from hipMalloc.  KP_POOL_SCORES=0 disables the pool.
+static std::atomic<bool> g_pool_touched[64];
+
+__global__ void kp_fill_pattern(uint32_t *p, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        p[i] = (uint32_t)(i * 2654435761u) ^ 0x5bd1e995u;
+}
+
+__global__ void kp_check_pattern(const uint32_t *p, size_t n, unsigned long long *bad) {
+    unsigned long long b = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        b += (p[i] != ((uint32_t)(i * 2654435761u) ^ 0x5bd1e995u));
+    for (int off = 32; off > 0; off >>= 1) b += __shfl_xor(b, off, 64);
+    if ((threadIdx.x & 63u) == 0 && b) atomicAdd(bad, b);
+}
+
+static void free_scores(kp_plan *p) {
+    if (!p->d_S) return;
+    if (p->S_pool) {
+        (void)hipFreeAsync(p->d_S, p->ctx->stream);
+        (void)hipStreamSynchronize(p->ctx->stream);
+    } else {
+        (void)hipFree(p->d_S);
+    }
+    p->d_S = nullptr;
+    p->S_pool = false;
+}
+
+static int alloc_scores(kp_plan *p, size_t bytes) {
+    kp_ctx *c = p->ctx;
+    const char *e = getenv("KP_POOL_SCORES");
+    const bool allow = !(e && atoi(e) == 0) && c->device >= 0 && c->device < 64;
+    if (allow && !g_pool_touched[c->device].exchange(true)) {
+        void *q = nullptr;
+        if (hipMallocAsync(&q, bytes, c->stream) == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess) {
+            unsigned long long *d_bad = nullptr, bad = 1;
+            const size_t n = bytes / 4;
+            if (hipMalloc(&d_bad, sizeof(bad)) == hipSuccess &&
+                hipMemsetAsync(d_bad, 0, sizeof(bad), c->stream) == hipSuccess) {
+                hipLaunchKernelGGL(kp_fill_pattern, dim3(16384), dim3(256), 0, c->stream, (uint32_t *)q, n);
+                hipLaunchKernelGGL(kp_check_pattern, dim3(16384), dim3(256), 0, c->stream, (const uint32_t *)q, n,
+                                   d_bad);
+                if (hipMemcpyAsync(&bad, d_bad, sizeof(bad), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                    hipStreamSynchronize(c->stream) != hipSuccess)
+                    bad = 1;
+            }
+            if (d_bad) (void)hipFree(d_bad);
+            if (bad == 0) {
+                p->d_S = static_cast<float *>(q);
+                p->S_pool = true;
+                return KP_OK;
+            }
+            (void)hipFreeAsync(q, c->stream);
+            (void)hipStreamSynchronize(c->stream);
+        }
+        (void)hipGetLastError();  // fall back to hipMalloc below
+    }
+    KP_HIP(dmalloc(&p->d_S, bytes));
+    p->S_pool = false;
+    return KP_OK;
+}
+
 static int ensure_lanes(kp_plan *p, uint64_t lanes) {
     if (lanes <= p->lanes_cap) return KP_OK;
     const kp::host_plan &hp = p->hp;
     const uint32_t ncap = node_cap_of(hp);
-    dfree(p->d_S);
+    free_scores(p);
     dfree(p->d_nodes);
     p->d_S = nullptr;
     p->d_nodes = nullptr;
@@ -671,7 +744,7 @@ static int ensure_lanes(kp_plan *p, uint64_t lanes) {
     KP_HIP(hipMemGetInfo(&fr, &tot));
     if (sb + nb + (256u << 20) > fr)
         return fail(KP_E_NOMEM, "lanes need " + std::to_string(sb + nb) + " bytes, free " + std::to_string(fr));
-    KP_HIP(dmalloc(&p->d_S, sb));
+    if (int rc = alloc_scores(p, sb)) return rc;
     KP_HIP(dmalloc(&p->d_nodes, nb));
     p->lanes_cap = lanes;
     p->node_cap = ncap;
@@ -940,7 +1013,7 @@ int kp_reserve_lanes(kp_plan *p, uint32_t lanes) {
     KP_HIP(hipSetDevice(p->ctx->device));
     const uint64_t had = p->lanes_cap;
     if (int rc = ensure_lanes(p, lanes)) return rc;
-    if (p->lanes_cap != had) {  // fault the new pages in now rather than in the first pass
+    if (p->lanes_cap != had && !p->S_pool) {  // fault the new pages in now rather than in the first pass
         KP_HIP(hipMemsetAsync(p->d_S, 0, p->hp.g.nblocks * (size_t)p->lanes_cap * p->hp.g.Bpad * 4, p->ctx->stream));
         KP_HIP(hipStreamSynchronize(p->ctx->stream));
     }
