@@ -135,3 +135,44 @@ def test_engine_run_groups_lane_granular_over_devices(monkeypatch):
         for v in ran.values():
             per_dev[v[0]] = per_dev.get(v[0], 0) + 1
         assert sorted(per_dev) == sorted(devs) and max(per_dev.values()) - min(per_dev.values()) <= 1
+
+
+def test_cv_driver_prepares_devices_during_fold_split():
+    """cv_roots hands the run_groups' prepare hook the lane shape of the grid (before the
+    fold split, so betas are placeholders) exactly once, and the roots are unchanged."""
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    from tests.emu import emu as E
+    c = golden_json("small_dp.json")["cases"]["k3"]
+    ctx = {k: tuple(v) for k, v in c["contextD"].items()}
+    seen = []
+
+    def run(gen_pat, M, U, groups, devices=None, max_block=0):
+        return E.run_groups(gen_pat, M, U, groups, devices=devices, max_block=max_block)
+
+    def prepare(gen_pat, groups, devices=None, max_block=0):
+        seen.append((gen_pat, [(g[0], g[1], list(g[3])) for g in groups]))
+    run.prepare = prepare
+    ref = cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], 1, np.uint32,
+                       run_groups=E.run_groups)
+    res = cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], 1, np.uint32,
+                       run_groups=run)
+    assert res["train"].tobytes() == ref["train"].tobytes() and res["test"].tobytes() == ref["test"].tobytes()
+    assert len(seen) == 1 and seen[0][0] == c["gen_pat"]
+    assert seen[0][1] == [(f, a, list(c["penalties"])) for a in c["alphas"] for f in range(c["nfolds"])]
+
+
+def test_cv_driver_prepare_errors_surface():
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    from tests.emu import emu as E
+    c = golden_json("small_dp.json")["cases"]["k3"]
+    ctx = {k: tuple(v) for k, v in c["contextD"].items()}
+
+    def run(gen_pat, M, U, groups, devices=None, max_block=0):
+        return E.run_groups(gen_pat, M, U, groups, devices=devices, max_block=max_block)
+
+    def prepare(gen_pat, groups, devices=None, max_block=0):
+        raise MemoryError("lattice does not fit")
+    run.prepare = prepare
+    with pytest.raises(MemoryError):
+        cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], 1, np.uint32,
+                     run_groups=run)
