@@ -201,52 +201,76 @@ def cv_shares(prep, world, cap):
     return [pack_passes(rank_groups(prep["groups"], r, world), cap) for r in range(world)]
 
 
-def full_cv(plan, prep, gen_pat, rank, world, cap, model_world=8):
-    """The whole grid x folds as the CV driver runs it: fold split (host C++), count tables,
-    this rank's lane-granular share of the passes, root read-out; on the plan the timed
-    steps used, whose lane buffers are already allocated.  The plan's table build runs
-    beside the fold split as in the CV driver (a second build is timed there); the
-    one-time HBM allocation is not in the wall-clock
-    (``prep["t_alloc"]``, reported beside it: on this platform it is dominated by the
-    driver wiping HBM that earlier processes freed, 0.05-6 s for 150 GB).  At world 1 it
-    also runs the shares the ``model_world`` ranks of an 8-GPU job would get, one after the
-    other, and models that job's wall-clock as the serial setup plus the slowest share
-    (there is no data-path collective)."""
+def cv_run(plan, prep, gen_pat, groups):
+    """One job's CV work as the CV driver runs it (cv_roots with the engine): all-data
+    counts in k-mer order, the fold split drawn on a host thread and handed over fold by
+    fold (CV_tools.fold_stream -> engine.FoldFeed), the plan's table build beside it (a
+    second build, timed), then ``groups``' passes in fold order, each fold uploaded when
+    it arrives (engine.run_groups).  Lane buffers are already allocated (the one-time
+    allocation is reported separately).  Returns the wall-clock and its parts."""
     import threading
-    from kmerpapa_amd.CV_tools import fold_tables as _ft
-    # the CV driver builds the plan's tables while the host draws the fold split
-    # (cv_roots -> engine.prepare_groups): time that overlap with a second table build
+    from kmerpapa_amd.CV_tools import all_counts, fold_stream
+    nf, itype, nk = prep["nfolds"], prep["itype"], plan.info["n_kmers"]
     box = {}
+    t0 = time.perf_counter()
 
     def tables():
         box["p"] = engine.Plan(plan.device, gen_pat, 0)
-        box["t"] = time.perf_counter() - t0
-    t0 = time.perf_counter()
+        box["t_tables"] = time.perf_counter() - t0
     th = threading.Thread(target=tables)
     th.start()
-    contexts, Mf, Uf = _ft(prep["ctx"], prep["nfolds"], np.random.RandomState(1), prep["itype"])
-    t_split = time.perf_counter() - t0
-    th.join()
-    t_tables = box["t"]
-    Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, plan.info["n_kmers"], prep["itype"])
-    plan.set_counts(Mk, Uk)
-    t_setup = time.perf_counter() - t0
-    box["p"].close()
+    contexts, Ma, Ua = all_counts(prep["ctx"], itype)
+    idx = engine.kmer_order(gen_pat, contexts)
+    M_all = np.zeros(nk, itype)
+    U_all = np.zeros(nk, itype)
+    M_all[idx] = Ma
+    U_all[idx] = Ua
+    feed = engine.FoldFeed(M_all, U_all, nf)
 
-    def share(passes):
-        ts = time.perf_counter()
-        for p in passes:
-            plan.run(p)
-        return time.perf_counter() - ts, sum(len(g[3]) for p in passes for g in p)
-    t_mine, lanes_mine = share(cv_shares(prep, world, cap)[rank])
-    out = {"wall_s": t_setup + t_mine, "setup_s": t_setup, "plan_tables_s": t_tables, "fold_split_s": t_split,
-           "passes_s": t_mine, "lanes": lanes_mine, "hbm_alloc_s": prep["t_alloc"],
-           "wall_s_incl_alloc": t_setup + t_mine + prep["t_alloc"]}
+    def produce():
+        try:
+            for f, Mf, Uf in fold_stream(prep["ctx"], nf, np.random.RandomState(1), itype):
+                mk = np.zeros(nk, itype)
+                uk = np.zeros(nk, itype)
+                mk[idx] = Mf
+                uk[idx] = Uf
+                feed.put(f, mk, uk)
+                box.setdefault("t_fold", []).append(time.perf_counter() - t0)
+        except BaseException as e:
+            feed.fail(e)
+    pr = threading.Thread(target=produce)
+    pr.start()
+    th.join()
+    t_start = time.perf_counter() - t0
+    engine.run_groups(gen_pat, feed, None, groups, devices=[plan.device.device])
+    pr.join()
+    wall = time.perf_counter() - t0
+    box["p"].close()
+    return {"wall_s": wall, "plan_tables_s": box["t_tables"], "fold_ready_s": [round(x, 4) for x in box["t_fold"]],
+            "fold_split_s": box["t_fold"][-1], "passes_start_s": t_start, "lanes": sum(len(g[3]) for g in groups)}
+
+
+def full_cv(plan, prep, gen_pat, rank, world, cap, model_world=8):
+    """The whole grid x folds as the CV driver runs it (cv_run: pipelined fold split,
+    this rank's lane-granular share of the passes in fold order, root read-out) on the plan
+    the timed steps used.  The one-time HBM allocation is not in the wall-clock
+    (``prep["t_alloc"]``, reported beside it: on this platform it is dominated by the
+    driver wiping HBM that earlier processes freed, 0.05-6 s for 150 GB).  At world 1 it
+    also runs, one after the other on the same GPU, the shares the ``model_world`` ranks
+    of an 8-GPU job would get -- each with its own pipelined fold split, as every rank
+    draws it -- and models that job's wall-clock as the slowest share (there is no
+    data-path collective)."""
+    from kmerpapa_amd.shard import rank_groups
+    out = cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], rank, world))
+    out["hbm_alloc_s"] = prep["t_alloc"]
+    out["wall_s_incl_alloc"] = out["wall_s"] + prep["t_alloc"]
     if world == 1 and model_world > 1:
-        shares = [share(p) for p in cv_shares(prep, model_world, cap)]
-        out["model"] = {"world": model_world, "share_s": [round(x[0], 4) for x in shares],
-                        "share_lanes": [x[1] for x in shares],
-                        "wall_s": t_setup + max(x[0] for x in shares)}
+        shares = [cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], r, model_world))
+                  for r in range(model_world)]
+        out["model"] = {"world": model_world, "share_s": [round(x["wall_s"], 4) for x in shares],
+                        "share_lanes": [x["lanes"] for x in shares],
+                        "share_passes_start_s": [round(x["passes_start_s"], 4) for x in shares],
+                        "wall_s": max(x["wall_s"] for x in shares)}
     return out
 
 

@@ -21,8 +21,10 @@
  *                    handle_pattern :26-78 for every cell) and its root read-out
  *                    :158-163; with fold = -1 the Fit sweep Fit :106-120
  *   kp_fit_leaves    backtrack(gen_pat, ...) Fit :17-24, 121
+ *   kp_counts_begin / kp_counts_fold   the same, one fold at a time
  *   kp_fold_split    CV_tools.py sample :5-27 and the fold loop of
- *                    make_all_folds_contextD_patterns :44-57 (host code, numpy legacy RNG)
+ *                    make_all_folds_contextD_patterns :44-57 (host code, numpy legacy RNG);
+ *                    kp_fold_sample: one fold of it (sample :5-27)
  *   kp_kmer_parse    io_utils.py read_dict :82-136 (with downsize_contextD's centring,
  *                    :50-79) and read_joint_kmer_counts :3-46 (host code)
  */
@@ -99,6 +101,15 @@ int kp_plan_get_info(const kp_plan *plan, kp_plan_info *out);
  * index = position in code[g]).  Builds the per-block k-mer-low count tables. */
 int kp_set_counts(kp_plan *plan, const void *M, const void *U, uint64_t n_kmers, int nf, int itype_bytes);
 
+/* The same tables fold by fold, so that passes can start while the host still draws the
+ * later folds (the CV driver's pipelined fold split).  kp_counts_begin: M_all, U_all
+ * [n_kmers] = counts of all data (the sum of the folds to come; the train counts of fold f
+ * are all data minus fold f, CV :22-24); it discards any fold set before.
+ * kp_counts_fold: M_fold, U_fold [n_kmers] = fold `fold`'s counts.  kp_pass refuses a
+ * group whose fold has not been set (KP_E_STATE). */
+int kp_counts_begin(kp_plan *plan, const void *M_all, const void *U_all, uint64_t n_kmers, int nf, int itype_bytes);
+int kp_counts_fold(kp_plan *plan, int fold, const void *M_fold, const void *U_fold, uint64_t n_kmers);
+
 /* One DP sweep of every lane of every group over the whole lattice.
  * Lanes are numbered group-major; per lane the outputs are the root's train score
  * (f32, as stored by the reference), the root's test -2LL (CV) and the number of
@@ -130,6 +141,10 @@ int kp_dump_lane(kp_plan *plan, uint32_t lane, float *score, uint8_t *code);
  * colors[n] = ball counts per colour; folds[n][nf] receives each colour's fold counts
  * (folds 0..nf-2 sampled, the last takes the remainder). */
 int kp_fold_split(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uint64_t n, int nf, uint64_t *folds);
+/* One fold of that split: CV_tools.py sample :5-27 (m balls drawn colour by colour from
+ * colors[n]; out[n] = the balls drawn of each colour), same RNG state convention. */
+int kp_fold_sample(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uint64_t n, uint64_t m,
+                   uint64_t *out);
 
 /* k-mer count text (host code, no GPU).  Parses `nbytes` of file text into a table of
  * unique k-mers as 2-bit codes (A=0 C=1 G=2 T=3, first letter most significant: code

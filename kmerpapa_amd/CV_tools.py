@@ -64,16 +64,12 @@ def _split_colors_numpy(colors, n_folds, itype, prng):
     return folds
 
 
-def fold_tables(contextD, n_folds, prng, itype=np.uint64):
-    """Fold counts per k-mer, in sorted-context order.
-
-    Returns ``(contexts, M, U)`` with ``M, U`` of shape ``[n_kmers, n_folds]``: exactly the
-    level-0 rows :func:`make_all_folds_contextD_patterns` scatters into ``M_mem``/``U_mem``.
-    """
+def _colors(contextD, itype):
+    """Contexts in sorted order and the urn of :func:`make_all_folds_contextD_patterns`
+    (ref :44-50): M counts of every context, then U counts."""
     if hasattr(contextD, "letters"):  # io_utils.KmerCounts: already in sorted order, as arrays
         contexts = contextD
         colors = np.concatenate([contextD.M, contextD.U]).astype(itype)
-        nk = len(contexts)
     else:
         contexts = sorted(contextD)
         nk = len(contexts)
@@ -82,8 +78,45 @@ def fold_tables(contextD, n_folds, prng, itype=np.uint64):
             nm, nu = contextD[c]
             colors[i] = nm
             colors[nk + i] = nu
+    return contexts, colors
+
+
+def fold_tables(contextD, n_folds, prng, itype=np.uint64):
+    """Fold counts per k-mer, in sorted-context order.
+
+    Returns ``(contexts, M, U)`` with ``M, U`` of shape ``[n_kmers, n_folds]``: exactly the
+    level-0 rows :func:`make_all_folds_contextD_patterns` scatters into ``M_mem``/``U_mem``.
+    """
+    contexts, colors = _colors(contextD, itype)
+    nk = len(contexts)
     folds = _split_colors(colors, n_folds, itype, prng)
     return contexts, folds[:nk], folds[nk:]
+
+
+def all_counts(contextD, itype=np.uint64):
+    """``(contexts, M, U)``: every context's counts of all data, in :func:`fold_tables`'
+    order (the sum of its folds)."""
+    contexts, colors = _colors(contextD, itype)
+    nk = len(contexts)
+    return contexts, colors[:nk], colors[nk:]
+
+
+def fold_stream(contextD, n_folds, prng, itype=np.uint64):
+    """:func:`fold_tables` one fold at a time: yields ``(f, M_f, U_f)`` (``[n_kmers]``,
+    sorted-context order) for f = 0 .. n_folds-1 as each fold is drawn, the same draws
+    from the same stream (each fold is one :func:`sample` in C++, ``kp_fold_sample``; the
+    last fold takes what is left).  The CV driver starts the GPU passes of fold 0 while
+    the later folds are still being drawn."""
+    from . import engine
+    contexts, colors = _colors(contextD, itype)
+    nk = len(contexts)
+    col = colors.astype(np.uint64)
+    per_fold = int(col.sum()) // n_folds  # n_samples = n // n_folds (ref :51)
+    for f in range(n_folds - 1):
+        s = engine.fold_sample(col, per_fold, prng)
+        col -= s
+        yield f, s[:nk].astype(itype), s[nk:].astype(itype)
+    yield n_folds - 1, col[:nk].astype(itype), col[nk:].astype(itype)
 
 
 def make_all_folds_contextD_patterns(contextD, U_mem, M_mem, general_pattern, prng, itype=np.uint64):

@@ -19,7 +19,7 @@ import threading
 import numpy as np
 
 from .. import engine
-from ..CV_tools import fold_tables
+from ..CV_tools import all_counts, fold_stream, fold_tables
 from ..pattern_utils import code, generality, pattern_level, perm_code
 from ..score_utils import get_betas
 
@@ -45,8 +45,14 @@ def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, ity
     Returns a dict with arrays ``train``/``test`` of shape
     ``[iterations, n_alpha, n_penalty, nfolds]`` (float32) and ``betas``
     ``[iterations, n_alpha, nfolds]``.  ``run_groups`` defaults to the GPU engine.
+
+    With a runner that takes fold-by-fold counts (``run_groups.fold_feed``, the engine's),
+    the fold split is drawn on a host thread (CV_tools.fold_stream) and handed over fold by
+    fold (engine.FoldFeed): the GPUs start on fold 0 while the later folds are drawn, and
+    a fold's betas are computed when it arrives.  Same draws, same numbers.
     """
     run_groups = run_groups or engine.run_groups
+    pipelined = bool(getattr(run_groups, "fold_feed", False))
     prng = np.random.RandomState(seed)
     na, nc = len(alphas), len(penalties)
     train = np.zeros((iterations, na, nc, nfolds), np.float32)
@@ -60,12 +66,12 @@ def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, ity
         if verbose > 0 and iterations > 1:
             print('CV Iteration', it, file=sys.stderr)
         th = None
+        box = {}
         if prepare is not None and it == 0:
             # the GPUs' lattice tables and lane buffers are set up while the host draws the
             # fold split (the native split releases the GIL); only lane counts matter here
             shape = [(f, a, 1.0, list(penalties[c0:c0 + engine.MAX_GROUP_LANES]))
                      for a in alphas for f in range(nfolds) for c0 in range(0, nc, engine.MAX_GROUP_LANES)]
-            box = {}
 
             def _prep():
                 try:
@@ -74,43 +80,99 @@ def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, ity
                     box["error"] = e
             th = threading.Thread(target=_prep)
             th.start()
-        try:
-            contexts, Mf, Uf = fold_tables(contextD, nfolds, prng, itype)
-        finally:
-            if th is not None:
-                th.join()
-        if th is not None and "error" in box:
-            raise box["error"]
-        if verbose > 0:
-            print('CV sampling DONE', file=sys.stderr)
-        Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, n_kmers, itype)
         # fold totals = column sums of M_mem over ALL rows (CV :134-137).  From the
         # second iteration on, the aggregated rows still hold the previous iteration's
         # sums: every k-mer count of the previous split appears once per containing
         # cell other than the k-mer itself.  Reproduced as the reference computes it.
-        M_sum = Mk.sum(axis=0, dtype=np.uint64)
-        U_sum = Uk.sum(axis=0, dtype=np.uint64)
+        carryM = np.zeros(nfolds, np.uint64)
+        carryU = np.zeros(nfolds, np.uint64)
         if prevM is not None:
             if mult is None:
                 mult = _cells_per_kmer(gen_pat) - np.uint64(1)
-            M_sum = M_sum + (prevM.astype(np.uint64) * mult[:, None]).sum(axis=0, dtype=np.uint64)
-            U_sum = U_sum + (prevU.astype(np.uint64) * mult[:, None]).sum(axis=0, dtype=np.uint64)
-        M_train = M_sum.sum() - M_sum
-        U_train = U_sum.sum() - U_sum
+            carryM = (prevM.astype(np.uint64) * mult[:, None]).sum(axis=0, dtype=np.uint64)
+            carryU = (prevU.astype(np.uint64) * mult[:, None]).sum(axis=0, dtype=np.uint64)
+        producer = None
+        try:
+            if pipelined:
+                contexts, Ma, Ua = all_counts(contextD, itype)
+                idx = engine.kmer_order(gen_pat, contexts if hasattr(contexts, "letters") else list(contexts))
+                M_all = np.zeros(n_kmers, itype)
+                U_all = np.zeros(n_kmers, itype)
+                M_all[idx] = Ma
+                U_all[idx] = Ua
+                feed = engine.FoldFeed(M_all, U_all, nfolds)
+
+                def _produce(feed=feed, idx=idx):
+                    try:
+                        for f, Mf, Uf in fold_stream(contextD, nfolds, prng, itype):
+                            mk = np.zeros(n_kmers, itype)
+                            uk = np.zeros(n_kmers, itype)
+                            mk[idx] = Mf
+                            uk[idx] = Uf
+                            feed.put(f, mk, uk)
+                        if verbose > 0:
+                            print('CV sampling DONE', file=sys.stderr)
+                    except BaseException as e:  # the GPU side raises it from feed.get
+                        feed.fail(e)
+                producer = threading.Thread(target=_produce)
+                producer.start()
+                M_tot = M_all.sum(dtype=np.uint64) + carryM.sum(dtype=np.uint64)  # = M_sum.sum()
+                U_tot = U_all.sum(dtype=np.uint64) + carryU.sum(dtype=np.uint64)
+                counts_M, counts_U = feed, None
+            else:
+                contexts, Mf, Uf = fold_tables(contextD, nfolds, prng, itype)
+                if verbose > 0:
+                    print('CV sampling DONE', file=sys.stderr)
+                Mk, Uk = engine.counts_in_kmer_order(gen_pat, contexts, Mf, Uf, n_kmers, itype)
+                M_sum = Mk.sum(axis=0, dtype=np.uint64) + carryM
+                U_sum = Uk.sum(axis=0, dtype=np.uint64) + carryU
+                counts_M, counts_U = Mk, Uk
+        finally:
+            if th is not None:
+                th.join()
+        if th is not None and "error" in box:
+            if producer is not None:
+                producer.join()
+            raise box["error"]
+
+        lock = threading.Lock()
+        cache = {}
+
+        def fold_betas(f, feed=counts_M if pipelined else None):
+            """Betas of fold f for every alpha (CV :138-141): get_betas over the fold's
+            train totals M_sum.sum() - M_sum[f] (uint64, as the reference)."""
+            with lock:
+                if f not in cache:
+                    if feed is not None:
+                        Mfk, Ufk = feed.get(f)
+                        mtr = np.array([M_tot - (Mfk.sum(dtype=np.uint64) + carryM[f])], np.uint64)
+                        utr = np.array([U_tot - (Ufk.sum(dtype=np.uint64) + carryU[f])], np.uint64)
+                    else:
+                        mtr = (M_sum.sum() - M_sum)[f:f + 1]
+                        utr = (U_sum.sum() - U_sum)[f:f + 1]
+                    cache[f] = [float(get_betas(alpha, mtr, utr)[0]) for alpha in alphas]
+                return cache[f]
+
         groups, where = [], []
         for a_i, alpha in enumerate(alphas):
-            betas = get_betas(alpha, M_train, U_train)
-            betas_all[it, a_i] = betas
             for f in range(nfolds):
+                beta = (lambda a_i=a_i, f=f: fold_betas(f)[a_i]) if pipelined else fold_betas(f)[a_i]
                 for c0 in range(0, nc, engine.MAX_GROUP_LANES):
                     chunk = list(penalties[c0:c0 + engine.MAX_GROUP_LANES])
-                    groups.append((f, alpha, float(betas[f]), chunk))
+                    groups.append((f, alpha, beta, chunk))
                     where.extend((a_i, c0 + j, f) for j in range(len(chunk)))
-        rt, re, _ = run_groups(gen_pat, Mk, Uk, groups, devices=devices, max_block=max_block)
+        try:
+            rt, re, _ = run_groups(gen_pat, counts_M, counts_U, groups, devices=devices, max_block=max_block)
+        finally:
+            if producer is not None:
+                producer.join()
+        for f in range(nfolds):
+            betas_all[it, :, f] = fold_betas(f)
         for lane, (a_i, p_i, f) in enumerate(where):
             train[it, a_i, p_i, f] = rt[lane]
             test[it, a_i, p_i, f] = re[lane]
-        prevM, prevU = Mk, Uk
+        if it + 1 < iterations:
+            prevM, prevU = counts_M.arrays() if pipelined else (counts_M, counts_U)
         if verbose > 0:
             _report(gen_pat, alphas, penalties, it, test[it], verbose)
     return {"train": train, "test": test, "betas": betas_all}

@@ -48,22 +48,24 @@
 // ---------------------------------------------------------------------------
 
 
+// Fills count slots s0 .. s0+ncol-1 of every block of high level H.  Kin_M/Kin_U are
+// [n_kmers][ncol] (k-mer order): column c goes to slot s0 + c.
 template <typename CT>
 __global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables T, uint64_t hbase, int H,
                                                         const CT *__restrict__ Kin_M, const CT *__restrict__ Kin_U,
-                                                        CT *__restrict__ K) {
+                                                        uint32_t ncol, uint32_t s0, CT *__restrict__ K) {
     const uint64_t h = T.hlist[hbase + blockIdx.x];
-    const uint32_t per = g.n_kl * (uint32_t)g.nf;
-    CT *dst = K + h * (uint64_t)per * 2;
+    const uint32_t S = kp_kslots(g);
+    CT *dst = K + h * (uint64_t)g.n_kl * S * 2;
     if (H == 0) {
         // all high digits are nucleotides: the block's k-mer-low cells are k-mers
         uint64_t kbase = 0;
         for (int i = 0; i < g.kh; ++i) kbase += (uint64_t)kp_high_digit(g, h, i) * g.khw[i];
-        for (uint32_t e = threadIdx.x; e < per; e += blockDim.x) {
-            uint32_t kl = e / (uint32_t)g.nf, f = e % (uint32_t)g.nf;
-            uint64_t src = (kbase + kl) * (uint64_t)g.nf + f;
-            dst[2 * e] = Kin_M[src];
-            dst[2 * e + 1] = Kin_U[src];
+        for (uint32_t e = threadIdx.x; e < g.n_kl * ncol; e += blockDim.x) {
+            const uint32_t kl = e / ncol, c = e % ncol;
+            const uint64_t src = (kbase + kl) * (uint64_t)ncol + c;
+            dst[2 * (kl * S + s0 + c)] = Kin_M[src];
+            dst[2 * (kl * S + s0 + c) + 1] = Kin_U[src];
         }
         return;
     }
@@ -79,9 +81,13 @@ __global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables
             break;
         }
     }
-    const CT *a = K + h1 * (uint64_t)per * 2;
-    const CT *b = K + h2 * (uint64_t)per * 2;
-    for (uint32_t e = threadIdx.x; e < 2 * per; e += blockDim.x) dst[e] = a[e] + b[e];
+    const CT *a = K + h1 * (uint64_t)g.n_kl * S * 2;
+    const CT *b = K + h2 * (uint64_t)g.n_kl * S * 2;
+    for (uint32_t e = threadIdx.x; e < g.n_kl * ncol * 2; e += blockDim.x) {
+        const uint32_t kl = e / (2 * ncol), r = e % (2 * ncol);
+        const uint32_t x = kl * S * 2 + 2 * s0 + r;
+        dst[x] = a[x] + b[x];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -376,9 +382,10 @@ struct kp_plan {
     uint8_t *d_lowmask = nullptr;
     uint32_t *d_lpairs = nullptr;
     // counts
-    void *d_K = nullptr;
+    void *d_K = nullptr;     // [h][kl][nf + 1][2] CT (kp_core.h)
     int nf = 0;
     int ct_bytes = 0;
+    std::vector<uint8_t> fold_set;  // fold f's slot holds counts (kp_counts_fold / kp_set_counts)
     // lanes
     float *d_S = nullptr;
     bool S_pool = false;  // d_S came from the device's stream-ordered pool (see alloc_scores)
@@ -548,18 +555,11 @@ int kp_plan_get_info(const kp_plan *p, kp_plan_info *o) {
 
 }  // extern "C"
 
+// (Re)allocate the count tables for nf folds (nf + 1 slots) and forget which folds are set.
 template <typename CT>
-static int run_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers, int nf) {
-    kp_ctx *c = p->ctx;
-    kp_geom g = p->hp.g;
-    g.nf = nf;
-    size_t in_bytes = n_kmers * (size_t)nf * sizeof(CT);
-    CT *dM = nullptr, *dU = nullptr;
-    KP_HIP(dmalloc(&dM, in_bytes));
-    KP_HIP(dmalloc(&dU, in_bytes));
-    KP_HIP(hipMemcpyAsync(dM, M, in_bytes, hipMemcpyHostToDevice, c->stream));
-    KP_HIP(hipMemcpyAsync(dU, U, in_bytes, hipMemcpyHostToDevice, c->stream));
-    size_t kbytes = g.nblocks * (size_t)g.n_kl * nf * 2 * sizeof(CT);
+static int counts_alloc(kp_plan *p, int nf) {
+    const kp_geom &g = p->hp.g;
+    size_t kbytes = g.nblocks * (size_t)g.n_kl * (nf + 1) * 2 * sizeof(CT);
     if (p->d_K && (p->nf != nf || p->ct_bytes != (int)sizeof(CT))) {
         dfree(p->d_K);
         p->d_K = nullptr;
@@ -567,26 +567,61 @@ static int run_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers
     if (!p->d_K) {
         size_t fr = 0, tot = 0;
         KP_HIP(hipMemGetInfo(&fr, &tot));
-        if (kbytes + (64u << 20) > fr) {
-            dfree(dM);
-            dfree(dU);
-            return fail(KP_E_NOMEM, "count tables need " + std::to_string(kbytes) + " bytes");
-        }
+        if (kbytes + (64u << 20) > fr) return fail(KP_E_NOMEM, "count tables need " + std::to_string(kbytes) + " bytes");
         KP_HIP(dmalloc(&p->d_K, kbytes));
     }
+    p->nf = nf;
+    p->ct_bytes = (int)sizeof(CT);
+    p->fold_set.assign(nf, 0);
+    return KP_OK;
+}
+
+// Fill slots s0 .. s0+ncol-1 from [n_kmers][ncol] host arrays (one launch per high level:
+// a level's aggregated rows sum two rows of lower levels).
+template <typename CT>
+static int counts_fill(kp_plan *p, const void *M, const void *U, uint32_t ncol, uint32_t s0) {
+    kp_ctx *c = p->ctx;
+    kp_geom g = p->hp.g;
+    g.nf = p->nf;
+    const size_t in_bytes = p->hp.n_kmers * (size_t)ncol * sizeof(CT);
+    CT *dM = nullptr, *dU = nullptr;
+    KP_HIP(dmalloc(&dM, in_bytes));
+    KP_HIP(dmalloc(&dU, in_bytes));
+    hipError_t e = hipMemcpyAsync(dM, M, in_bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dU, U, in_bytes, hipMemcpyHostToDevice, c->stream);
     kp_dev_tables T = tables_of(p);
-    for (int H = 0; H <= p->hp.hmax; ++H) {
+    for (int H = 0; H <= p->hp.hmax && e == hipSuccess; ++H) {
         uint64_t nb = p->hp.hoff[H + 1] - p->hp.hoff[H];
         if (!nb) continue;
         hipLaunchKernelGGL(kp_counts_kernel<CT>, dim3((unsigned)nb), dim3(256), 0, c->stream, g, T, p->hp.hoff[H], H,
-                           dM, dU, reinterpret_cast<CT *>(p->d_K));
-        KP_HIP(hipGetLastError());
+                           dM, dU, ncol, s0, reinterpret_cast<CT *>(p->d_K));
+        e = hipGetLastError();
     }
-    KP_HIP(hipStreamSynchronize(c->stream));
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dfree(dM);
     dfree(dU);
-    p->nf = nf;
-    p->ct_bytes = (int)sizeof(CT);
+    if (e != hipSuccess) return fail(KP_E_HIP, std::string("count tables: ") + hipGetErrorString(e));
+    return KP_OK;
+}
+
+// every fold at once: slot 0 = the sum over folds (exact in itype), slots 1.. = the folds
+template <typename CT>
+static int run_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers, int nf) {
+    const CT *m = static_cast<const CT *>(M), *u = static_cast<const CT *>(U);
+    std::vector<CT> tm(n_kmers), tu(n_kmers);
+    for (uint64_t i = 0; i < n_kmers; ++i) {
+        CT a = 0, b = 0;
+        for (int f = 0; f < nf; ++f) {
+            a += m[i * nf + f];
+            b += u[i * nf + f];
+        }
+        tm[i] = a;
+        tu[i] = b;
+    }
+    if (int rc = counts_alloc<CT>(p, nf)) return rc;
+    if (int rc = counts_fill<CT>(p, tm.data(), tu.data(), 1, 0)) return rc;
+    if (int rc = counts_fill<CT>(p, M, U, (uint32_t)nf, 1)) return rc;
+    std::fill(p->fold_set.begin(), p->fold_set.end(), (uint8_t)1);
     return KP_OK;
 }
 
@@ -601,6 +636,34 @@ int kp_set_counts(kp_plan *p, const void *M, const void *U, uint64_t n_kmers, in
     if (itype_bytes == 4) return run_counts<uint32_t>(p, M, U, n_kmers, nf);
     if (itype_bytes == 8) return run_counts<uint64_t>(p, M, U, n_kmers, nf);
     return fail(KP_E_ARG, "itype_bytes must be 4 or 8");
+}
+
+int kp_counts_begin(kp_plan *p, const void *M_all, const void *U_all, uint64_t n_kmers, int nf, int itype_bytes) {
+    if (!p || !M_all || !U_all) return fail(KP_E_ARG, "null argument");
+    if (n_kmers != p->hp.n_kmers)
+        return fail(KP_E_ARG, "n_kmers " + std::to_string(n_kmers) + " != " + std::to_string(p->hp.n_kmers));
+    if (nf < 1 || nf > 64) return fail(KP_E_ARG, "nf must be 1..64");
+    if (itype_bytes != 4 && itype_bytes != 8) return fail(KP_E_ARG, "itype_bytes must be 4 or 8");
+    KP_HIP(hipSetDevice(p->ctx->device));
+    if (itype_bytes == 4) {
+        if (int rc = counts_alloc<uint32_t>(p, nf)) return rc;
+        return counts_fill<uint32_t>(p, M_all, U_all, 1, 0);
+    }
+    if (int rc = counts_alloc<uint64_t>(p, nf)) return rc;
+    return counts_fill<uint64_t>(p, M_all, U_all, 1, 0);
+}
+
+int kp_counts_fold(kp_plan *p, int fold, const void *M_fold, const void *U_fold, uint64_t n_kmers) {
+    if (!p || !M_fold || !U_fold) return fail(KP_E_ARG, "null argument");
+    if (!p->d_K) return fail(KP_E_STATE, "kp_counts_begin must come first");
+    if (n_kmers != p->hp.n_kmers)
+        return fail(KP_E_ARG, "n_kmers " + std::to_string(n_kmers) + " != " + std::to_string(p->hp.n_kmers));
+    if (fold < 0 || fold >= p->nf) return fail(KP_E_ARG, "fold out of range");
+    KP_HIP(hipSetDevice(p->ctx->device));
+    int rc = p->ct_bytes == 4 ? counts_fill<uint32_t>(p, M_fold, U_fold, 1, 1u + (uint32_t)fold)
+                              : counts_fill<uint64_t>(p, M_fold, U_fold, 1, 1u + (uint32_t)fold);
+    if (rc == KP_OK) p->fold_set[fold] = 1;
+    return rc;
 }
 
 }  // extern "C"
@@ -771,6 +834,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         const kp_group &u = groups[i];
         if (u.n_lanes < 1 || u.n_lanes > KP_GROUP_MAX_LANES) return fail(KP_E_ARG, "group lanes must be 1..8");
         if (u.fold >= p->nf || u.fold < -1) return fail(KP_E_ARG, "fold out of range");
+        if (u.fold >= 0 && !p->fold_set[u.fold])
+            return fail(KP_E_STATE, "counts of fold " + std::to_string(u.fold) + " are not set (kp_counts_fold)");
         for (int s = 0; s < u.n_lanes; s += per_wg) {
             kp_group_dev d;
             memset(&d, 0, sizeof(d));
@@ -1061,6 +1126,26 @@ int kp_dump_lane(kp_plan *p, uint32_t lane, float *score, uint8_t *code) {
 }  // extern "C"
 
 extern "C" {
+
+int kp_fold_sample(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uint64_t n, uint64_t m,
+                   uint64_t *out) {
+    if (!mt_key || !mt_pos || (n && (!colors || !out))) return fail(KP_E_ARG, "bad arguments");
+    if (*mt_pos < 0 || *mt_pos > 624) return fail(KP_E_ARG, "MT19937 position out of range");
+    if (!n) return KP_OK;
+    kpf::mt19937 rng;
+    memcpy(rng.key, mt_key, sizeof(rng.key));
+    rng.pos = *mt_pos;
+    std::vector<uint64_t> tail(n);
+    uint64_t acc = 0;
+    for (uint64_t i = n; i-- > 0;) {
+        acc += colors[i];
+        tail[i] = acc;
+    }
+    kpf::sample(rng, m, colors, tail.data(), n, out);
+    memcpy(mt_key, rng.key, sizeof(rng.key));
+    *mt_pos = rng.pos;
+    return KP_OK;
+}
 
 int kp_fold_split(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uint64_t n, int nf, uint64_t *folds) {
     if (!mt_key || !mt_pos || (n && (!colors || !folds)) || nf < 1) return fail(KP_E_ARG, "bad arguments");

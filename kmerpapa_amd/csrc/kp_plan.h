@@ -282,11 +282,28 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     P.hmax = hmax;
     P.hoff.assign(hmax + 2, 0);
     if (g.nblocks > 0xFFFFFFFFull) return "too many blocks for 32-bit block ids";
+    if (g.kh > 15) return "too many high positions for packed digits";
+    // high levels of every block: a mixed-radix counter over h (high position 0 fastest)
+    // keeps the digits and their level sum, no 64-bit divisions (this runs on the host
+    // beside the fold split, before the first pass can start)
     std::vector<uint8_t> hl(g.nblocks);
-    for (uint64_t h = 0; h < g.nblocks; ++h) {
-        int s = kp_high_level(g, P.tabs.data(), h);
-        hl[h] = (uint8_t)s;
-        P.hoff[s + 1]++;
+    {
+        std::vector<uint32_t> dig(g.kh, 0);
+        int s = 0;
+        for (uint64_t h = 0; h < g.nblocks; ++h) {
+            hl[h] = (uint8_t)s;
+            P.hoff[s + 1]++;
+            for (int i = 0; i < g.kh; ++i) {
+                const kp_postab &T = P.tabs[g.t + i];
+                s -= T.lev[dig[i]];
+                if (++dig[i] < g.r[g.t + i]) {
+                    s += T.lev[dig[i]];
+                    break;
+                }
+                dig[i] = 0;
+                s += T.lev[0];
+            }
+        }
     }
     for (int s = 0; s <= hmax; ++s) P.hoff[s + 1] += P.hoff[s];
     P.hlist.resize(g.nblocks);
@@ -350,17 +367,23 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
                 if (j == g.kh) break;
             }
         } else {
+            // mixed-radix counter, perm[0] fastest; the packed digits come along
+            P.hdig.resize(g.nblocks);
             std::vector<uint32_t> dig(g.kh, 0);
-            uint64_t h = 0;
-            for (uint64_t n = 0; n < g.nblocks; ++n) {  // mixed-radix counter, perm[0] fastest
-                P.hlist[fill[hl[h]]++] = (uint32_t)h;
+            uint64_t h = 0, w = 0;
+            for (uint64_t n = 0; n < g.nblocks; ++n) {
+                const uint64_t q = fill[hl[h]]++;
+                P.hlist[q] = (uint32_t)h;
+                P.hdig[q] = w;
                 for (int j = 0; j < g.kh; ++j) {
                     const int i = perm[j];
                     if (++dig[i] < g.r[g.t + i]) {
                         h += g.hcg[i];
+                        w += 1ull << (4 * i);
                         break;
                     }
                     h -= (uint64_t)(dig[i] - 1) * g.hcg[i];
+                    w &= ~(15ull << (4 * i));
                     dig[i] = 0;
                 }
             }
@@ -368,6 +391,7 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
         for (int s = 0; s <= hmax; ++s)
             if (fill[s] != P.hoff[s + 1]) return "block order does not cover every block";
         const char *bo = getenv("KP_BLOCK_ORDER");
+        if (bo && atoi(bo) == 1) P.hdig.clear();  // recomputed below for the shuffled list
         if (bo && atoi(bo) == 1)
             for (int s = 0; s <= hmax; ++s) {  // experiment: shuffled (no reuse order)
                 uint32_t *b = P.hlist.data() + P.hoff[s], *e = P.hlist.data() + P.hoff[s + 1];
@@ -378,12 +402,13 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
                 }
             }
     }
-    if (g.kh > 15) return "too many high positions for packed digits";
-    P.hdig.resize(g.nblocks);
-    for (uint64_t q = 0; q < g.nblocks; ++q) {
-        uint64_t h = P.hlist[q], w = 0;
-        for (int i = 0; i < g.kh; ++i) w |= (uint64_t)kp_high_digit(g, h, i) << (4 * i);
-        P.hdig[q] = w;
+    if (P.hdig.size() != g.nblocks) {  // experiment orders (tiled, shuffled)
+        P.hdig.resize(g.nblocks);
+        for (uint64_t q = 0; q < g.nblocks; ++q) {
+            uint64_t h = P.hlist[q], w = 0;
+            for (int i = 0; i < g.kh; ++i) w |= (uint64_t)kp_high_digit(g, h, i) << (4 * i);
+            P.hdig[q] = w;
+        }
     }
     // split pairs per position: sum over digits of np, times the other radices
     for (int i = 0; i < k; ++i) {

@@ -13,6 +13,7 @@ Host-side responsibilities kept here:
   * sharding: groups are spread over the visible GPUs, one host thread per GPU
     (ctypes releases the GIL during every call), no collective needed.
 """
+import atexit
 import ctypes
 import os
 import threading
@@ -58,9 +59,9 @@ class KPPassStats(ctypes.Structure):
 
 
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
-           "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_pass", "kp_reserve_lanes", "kp_last_pass_stats",
-           "kp_fit_leaves", "kp_dump_lane", "kp_fold_split", "kp_kmer_parse", "kp_kmer_table_info",
-           "kp_kmer_table_copy", "kp_kmer_table_free"]
+           "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
+           "kp_reserve_lanes", "kp_last_pass_stats", "kp_fit_leaves", "kp_dump_lane", "kp_fold_split",
+           "kp_fold_sample", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free"]
 
 
 def load():
@@ -93,12 +94,15 @@ def load():
         L.kp_kmer_table_free.argtypes = [vp]
         L.kp_kmer_table_free.restype = None
         L.kp_set_counts.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.kp_counts_begin.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.kp_counts_fold.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_uint64]
         L.kp_pass.argtypes = [vp, ctypes.POINTER(KPGroup), ctypes.c_int, vp, vp, vp]
         L.kp_last_pass_stats.argtypes = [vp, ctypes.POINTER(KPPassStats)]
         L.kp_reserve_lanes.argtypes = [vp, ctypes.c_uint32]
         L.kp_fit_leaves.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u64p]
         L.kp_dump_lane.argtypes = [vp, ctypes.c_uint32, vp, vp]
         L.kp_fold_split.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_int, vp]
+        L.kp_fold_sample.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_uint64, vp]
         for name in EXPORTS:
             if name not in ("kp_destroy", "kp_plan_destroy", "kp_last_error", "kp_kmer_table_free"):
                 getattr(L, name).restype = ctypes.c_int
@@ -152,6 +156,24 @@ def fold_split(colors, n_folds, prng):
     out = np.zeros((col.shape[0], int(n_folds)), dtype=np.uint64)
     _check(L.kp_fold_split(_ptr(key), ctypes.byref(pos), _ptr(col), ctypes.c_uint64(col.shape[0]), int(n_folds),
                            _ptr(out)))
+    prng.set_state((st[0], key, pos.value, st[3], st[4]))
+    return out
+
+
+def fold_sample(colors, m, prng):
+    """One fold of the split: ``m`` balls drawn colour by colour from ``colors``
+    (CV_tools.py sample :5-27) with the caller's numpy ``RandomState`` stream, in C++
+    (``kp_fold_sample``).  Returns uint64 ``[n]``; ``prng`` advances as numpy's would."""
+    L = load()
+    st = prng.get_state(legacy=True)
+    if st[0] != "MT19937":
+        raise ValueError("fold split needs a legacy MT19937 RandomState")
+    key = np.array(st[1], dtype=np.uint32)
+    pos = ctypes.c_int32(int(st[2]))
+    col = np.ascontiguousarray(colors, dtype=np.uint64)
+    out = np.zeros(col.shape[0], dtype=np.uint64)
+    _check(L.kp_fold_sample(_ptr(key), ctypes.byref(pos), _ptr(col), ctypes.c_uint64(col.shape[0]),
+                            ctypes.c_uint64(int(m)), _ptr(out)))
     prng.set_state((st[0], key, pos.value, st[3], st[4]))
     return out
 
@@ -253,8 +275,27 @@ class Plan:
         self.nf = M.shape[1]
         self.itype = M.dtype
 
+    def counts_begin(self, M_all, U_all, nf):
+        """Start a fold-by-fold count upload: ``M_all``/``U_all`` ``[n_kmers]`` = counts of
+        all data in k-mer order (uint32/uint64), ``nf`` folds to come (kp_counts_begin)."""
+        M_all = np.ascontiguousarray(M_all).reshape(-1)
+        if M_all.dtype not in (np.uint32, np.uint64):
+            raise TypeError("counts must be uint32 or uint64")
+        U_all = np.ascontiguousarray(U_all, dtype=M_all.dtype).reshape(-1)
+        _check(load().kp_counts_begin(self._h, _ptr(M_all), _ptr(U_all), ctypes.c_uint64(M_all.shape[0]), int(nf),
+                                      int(M_all.dtype.itemsize)))
+        self.nf = int(nf)
+        self.itype = M_all.dtype
+
+    def counts_fold(self, fold, M_fold, U_fold):
+        """Counts of one fold ``[n_kmers]`` (same itype as counts_begin; kp_counts_fold)."""
+        M_fold = np.ascontiguousarray(M_fold, dtype=self.itype).reshape(-1)
+        U_fold = np.ascontiguousarray(U_fold, dtype=self.itype).reshape(-1)
+        _check(load().kp_counts_fold(self._h, int(fold), _ptr(M_fold), _ptr(U_fold), ctypes.c_uint64(M_fold.shape[0])))
+
     def run(self, groups):
-        """One DP sweep.  ``groups``: list of ``(fold, alpha, beta, penalties)``.
+        """One DP sweep.  ``groups``: list of ``(fold, alpha, beta, penalties)``; ``beta`` may
+        be a callable returning it (the CV driver's betas of folds still being drawn).
 
         Returns ``(root_train f32[L], root_test f32[L], n_leaves u64[L])`` with lanes
         numbered group-major.
@@ -268,7 +309,7 @@ class Plan:
             arr[i].fold = int(fold)
             arr[i].n_lanes = len(pens)
             arr[i].alpha = float(alpha)
-            arr[i].beta = float(beta)
+            arr[i].beta = float(beta() if callable(beta) else beta)
             for j, c in enumerate(pens):
                 arr[i].penalty[j] = float(c)
             nl += len(pens)
@@ -367,6 +408,56 @@ def counts_in_kmer_order(gen_pat, contexts, M, U, n_kmers, itype):
     return outM, outU
 
 
+class FoldFeed:
+    """Fold counts that arrive one fold at a time, in k-mer order: the CV driver draws the
+    fold split on a host thread (CV_tools.fold_stream) while the GPUs already run the
+    passes of the folds drawn so far.  ``M_all``/``U_all`` ``[n_kmers]`` = counts of all
+    data (the sum of the folds to come), ``nf`` folds."""
+
+    def __init__(self, M_all, U_all, nf):
+        self.M_all = np.ascontiguousarray(M_all).reshape(-1)
+        self.U_all = np.ascontiguousarray(U_all, dtype=self.M_all.dtype).reshape(-1)
+        self.nf = int(nf)
+        self._cols = [None] * self.nf
+        self._err = None
+        self._cv = threading.Condition()
+
+    def put(self, fold, M_fold, U_fold):
+        with self._cv:
+            self._cols[fold] = (np.ascontiguousarray(M_fold, dtype=self.M_all.dtype),
+                                np.ascontiguousarray(U_fold, dtype=self.M_all.dtype))
+            self._cv.notify_all()
+
+    def fail(self, exc):
+        """The producer failed: every waiting and later ``get`` raises."""
+        with self._cv:
+            self._err = exc
+            self._cv.notify_all()
+
+    def get(self, fold):
+        """``(M_fold, U_fold)``, waiting until the fold has been drawn."""
+        with self._cv:
+            while self._cols[fold] is None and self._err is None:
+                self._cv.wait()
+            if self._cols[fold] is None:
+                raise RuntimeError(f"fold split failed before fold {fold}") from self._err
+            return self._cols[fold]
+
+    def arrays(self):
+        """``(M, U)`` ``[n_kmers, nf]`` once every fold has arrived."""
+        cols = [self.get(f) for f in range(self.nf)]
+        return np.stack([c[0] for c in cols], axis=1), np.stack([c[1] for c in cols], axis=1)
+
+
+def materialize(M, U, groups):
+    """For runners without fold-by-fold upload: wait for a FoldFeed's folds and resolve
+    callable betas.  Returns ``(M, U, groups)`` with arrays and float betas."""
+    if isinstance(M, FoldFeed):
+        M, U = M.arrays()
+    groups = [(f, a, float(b() if callable(b) else b), pens) for f, a, b, pens in groups]
+    return M, U, groups
+
+
 def pass_cap(groups, fit):
     """Lanes per pass: the largest group, if it fits.  Passes with more lanes are not faster
     per lane (each (alpha, fold) group is its own set of workgroups), but need more HBM,
@@ -418,10 +509,28 @@ def get_plan(dev, gen_pat, max_block=0):
 
 
 def release_all():
+    """Free every cached plan's device buffers (the devices stay open)."""
     with _cache_lock:
         for p in _plans.values():
             p.close()
         _plans.clear()
+
+
+def _shutdown():
+    """At interpreter exit, while the library and the HIP runtime are still loaded: plans
+    first (a plan's pooled score buffer is freed on its device's stream), then devices.
+    Left to garbage collection, module teardown may destroy a device before its plan."""
+    try:
+        release_all()
+        with _cache_lock:
+            for d in _devices.values():
+                d.close()
+            _devices.clear()
+    except Exception:
+        pass
+
+
+atexit.register(_shutdown)
 
 
 def _device_shares(groups, devices):
@@ -452,12 +561,14 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0):
 def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     """Run every lane group over the lattice of ``gen_pat`` on the given GPUs.
 
-    ``M``/``U`` are ``[n_kmers, nf]`` counts in k-mer order.  The lanes (one penalty of one
-    group, group-major) are cut into one contiguous, equal run per GPU and regrouped by
-    (fold, alpha) (``shard.rank_groups``, the same lane-granular split the ranks of a
-    torchrun job use), each GPU's share packed into memory-sized passes, one host thread
-    per GPU.  Returns ``(root_train, root_test, n_leaves)`` arrays over all lanes,
-    group-major.
+    ``M``/``U`` are ``[n_kmers, nf]`` counts in k-mer order, or ``M`` is a
+    :class:`FoldFeed` (``U`` unused): then every GPU uploads the all-data counts first and
+    each fold as it arrives, and runs its passes in fold order, so the first passes start
+    before the last folds are drawn.  The lanes (one penalty of one group, group-major)
+    are cut into one contiguous, equal run per GPU and regrouped by (fold, alpha)
+    (``shard.rank_groups``, the same lane-granular split the ranks of a torchrun job use),
+    each GPU's share packed into memory-sized passes, one host thread per GPU.  Returns
+    ``(root_train, root_test, n_leaves)`` arrays over all lanes, group-major.
     """
     devices = list(devices) if devices is not None else visible_devices()[:1]
     devices = list(dict.fromkeys(devices))  # one host thread per GPU: a device's plan is not shared
@@ -468,16 +579,29 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     results = [None] * nd
     errors = []
 
+    feed = M if isinstance(M, FoldFeed) else None
+
     def work(slot, dev, chunk):
         try:
             outs = []
             if chunk:
                 plan = get_plan(dev, gen_pat, max_block)
-                plan.set_counts(M, U)
+                if feed is not None:
+                    plan.counts_begin(feed.M_all, feed.U_all, feed.nf)
+                else:
+                    plan.set_counts(M, U)
                 passes = pack_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
                 plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))  # one allocation
-                for pas in passes:
-                    outs.append(plan.run(pas))
+                outs = [None] * len(passes)
+                # folds arrive in order: passes whose folds come first run first
+                order = sorted(range(len(passes)), key=lambda i: max(g[0] for g in passes[i]))
+                have = set()
+                for i in order:
+                    if feed is not None:
+                        for f in sorted({g[0] for g in passes[i] if g[0] >= 0} - have):
+                            plan.counts_fold(f, *feed.get(f))
+                            have.add(f)
+                    outs[i] = plan.run(passes[i])
             if outs:
                 results[slot] = tuple(np.concatenate([o[i] for o in outs]) for i in range(3))
             else:
@@ -502,3 +626,4 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
 
 
 run_groups.prepare = prepare_groups
+run_groups.fold_feed = True  # accepts a FoldFeed for M

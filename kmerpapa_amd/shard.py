@@ -71,6 +71,7 @@ def sharded_run_groups(run_groups, rank, world, all_gather, devices=None):
         parts = all_gather((np.asarray(rt), np.asarray(re), np.asarray(nl)))
         return tuple(np.concatenate([p[i] for p in parts]) for i in range(3))
     run.prepare = prepare
+    run.fold_feed = getattr(run_groups, "fold_feed", False)
     return run
 
 

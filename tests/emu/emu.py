@@ -63,6 +63,12 @@ def run(gen_pat, M, U, groups, max_block=4096, dump=False):
 
 
 def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
-    """Drop-in for kmerpapa_amd.engine.run_groups backed by the emulator (CPU tests only)."""
+    """Drop-in for kmerpapa_amd.engine.run_groups backed by the emulator (CPU tests only);
+    takes a FoldFeed for M like the engine (waits for every fold)."""
+    from kmerpapa_amd.engine import materialize
+    M, U, groups = materialize(M, U, groups)
     out = run(gen_pat, M, U, groups, max_block=max_block or 4096)
     return out["root_train"], out["root_test"], out["n_leaves"]
+
+
+run_groups.fold_feed = True

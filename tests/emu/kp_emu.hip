@@ -44,9 +44,9 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
     uint32_t Ltot = 0;
     for (int i = 0; i < ngroups; ++i) Ltot += (uint32_t)groups[i].nl;
     g.Ltot = Ltot;
-    const uint64_t per = (uint64_t)g.n_kl * nf * 2;
+    const uint64_t KS = kp_kslots(g), per = (uint64_t)g.n_kl * KS * 2;
     std::vector<CT> K(g.nblocks * per);
-    // counts (kp_counts_kernel)
+    // counts (kp_counts_kernel): slot 0 = all data (sum of the folds), slot 1 + f = fold f
     for (int H = 0; H <= hp.hmax; ++H) {
         for (uint64_t q = hp.hoff[H]; q < hp.hoff[H + 1]; ++q) {
             uint64_t h = hp.hlist[q];
@@ -54,10 +54,16 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
             if (H == 0) {
                 uint64_t kbase = 0;
                 for (int i = 0; i < g.kh; ++i) kbase += (uint64_t)kp_high_digit(g, h, i) * g.khw[i];
-                for (uint64_t e = 0; e < per / 2; ++e) {
-                    uint64_t kl = e / nf, f = e % nf;
-                    dst[2 * e] = M[(kbase + kl) * nf + f];
-                    dst[2 * e + 1] = U[(kbase + kl) * nf + f];
+                for (uint64_t kl = 0; kl < g.n_kl; ++kl) {
+                    CT am = 0, au = 0;
+                    for (int f = 0; f < nf; ++f) {
+                        dst[2 * (kl * KS + 1 + f)] = M[(kbase + kl) * nf + f];
+                        dst[2 * (kl * KS + 1 + f) + 1] = U[(kbase + kl) * nf + f];
+                        am += M[(kbase + kl) * nf + f];
+                        au += U[(kbase + kl) * nf + f];
+                    }
+                    dst[2 * kl * KS] = am;
+                    dst[2 * kl * KS + 1] = au;
                 }
             } else {
                 uint64_t h1 = h, h2 = h;

@@ -53,3 +53,23 @@ def test_fold_split_continues_the_callers_stream():
     for _ in range(3):
         assert np.array_equal(_split_colors_numpy(colors, 4, np.uint64, p1), engine.fold_split(colors, 4, p2))
     assert p1.randint(0, 2 ** 30) == p2.randint(0, 2 ** 30)
+
+
+@pytest.mark.parametrize("nf", [2, 3, 5, 10])
+def test_fold_stream_matches_fold_tables(nf):
+    """CV_tools.fold_stream (one kp_fold_sample per fold, the CV driver's pipelined split)
+    draws exactly fold_tables' folds and leaves the stream in the same state."""
+    from kmerpapa_amd.CV_tools import fold_stream, fold_tables
+    rng = np.random.RandomState(nf)
+    ctx = {}
+    for _ in range(400):
+        ctx["".join(rng.choice(list("ACGT"), 6))] = (int(rng.randint(0, 40)), int(rng.randint(0, 5000)))
+    for itype in (np.uint32, np.uint64):
+        p1, p2 = np.random.RandomState(11), np.random.RandomState(11)
+        _, M, U = fold_tables(ctx, nf, p1, itype)
+        got = list(fold_stream(ctx, nf, p2, itype))
+        assert [g[0] for g in got] == list(range(nf))
+        for f, Mf, Uf in got:
+            assert Mf.dtype == itype and np.array_equal(Mf, M[:, f]) and np.array_equal(Uf, U[:, f])
+        s1, s2 = p1.get_state(), p2.get_state()
+        assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]

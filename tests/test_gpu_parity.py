@@ -380,6 +380,15 @@ def test_error_paths(eng):
         plan.run([(0, 1.0, 1.0, [1.0])])  # no counts set
     with pytest.raises(ValueError):
         plan.run([(0, 1.0, 1.0, [1.0] * 9)])  # more than 8 penalties in a group
+    n = plan.info["n_kmers"]
+    plan.counts_begin(np.full(n, 5, np.uint32), np.full(n, 50, np.uint32), 3)
+    plan.run([(-1, 1.0, 1.0, [1.0])])  # fit mode needs only the all-data counts
+    with pytest.raises(eng.KPError, match="fold 1 are not set"):
+        plan.run([(1, 1.0, 1.0, [1.0])])
+    plan.counts_fold(1, np.full(n, 2, np.uint32), np.full(n, 20, np.uint32))
+    plan.run([(1, 1.0, 1.0, [1.0])])
+    with pytest.raises(eng.KPError, match="fold out of range"):
+        plan.counts_fold(3, np.zeros(n, np.uint32), np.zeros(n, np.uint32))
     plan.close()
     with pytest.raises(eng.KPError):
         eng.Plan(dev, "NXN", 0)  # not an IUPAC code

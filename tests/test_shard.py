@@ -176,3 +176,89 @@ def test_cv_driver_prepare_errors_surface():
     with pytest.raises(MemoryError):
         cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], 1, np.uint32,
                      run_groups=run)
+
+
+def test_cv_driver_pipelined_fold_split_same_roots():
+    """With a runner that takes a FoldFeed (fold-by-fold counts, lazy betas), cv_roots gives
+    bit-identical roots and betas to the runner that gets the whole split at once,
+    including the --iterations carry-over of the fold totals."""
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    from tests.emu import emu as E
+    c = golden_json("small_dp.json")["cases"]["k3"]
+    ctx = {k: tuple(v) for k, v in c["contextD"].items()}
+    calls = []
+
+    def whole(gen_pat, M, U, groups, devices=None, max_block=0):  # no fold_feed attribute
+        calls.append(type(M).__name__)
+        return E.run_groups(gen_pat, M, U, groups, devices=devices, max_block=max_block)
+
+    def fed(gen_pat, M, U, groups, devices=None, max_block=0):
+        calls.append(type(M).__name__)
+        return E.run_groups(gen_pat, M, U, groups, devices=devices, max_block=max_block)
+    fed.fold_feed = True
+    for it in (1, 2):
+        calls.clear()
+        a = cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], it, np.uint32,
+                         run_groups=whole)
+        b = cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], it, np.uint32,
+                         run_groups=fed)
+        assert calls == ["ndarray"] * it + ["FoldFeed"] * it
+        for key in ("train", "test", "betas"):
+            assert a[key].tobytes() == b[key].tobytes(), key
+
+
+def test_engine_run_groups_fold_feed_order(monkeypatch):
+    """engine.run_groups with a FoldFeed: all-data counts first, each fold uploaded once
+    before the first pass that needs it, passes in fold order, lazy betas resolved when a
+    pass runs, results in the original lane order; a failed split surfaces."""
+    import threading
+    from kmerpapa_amd import engine
+    log = []
+
+    class FakePlan:
+        def __init__(self, dev):
+            self.dev = dev
+
+        def counts_begin(self, M, U, nf):
+            log.append(("begin", nf))
+
+        def counts_fold(self, f, M, U):
+            log.append(("fold", f))
+
+        def lanes_that_fit(self):
+            return 5
+
+        def reserve(self, lanes):
+            pass
+
+        def run(self, groups):
+            for g in groups:
+                assert ("fold", g[0]) in log
+            b = [g[2]() if callable(g[2]) else g[2] for g in groups]
+            log.append(("pass", tuple(g[0] for g in groups)))
+            lanes = [(g[0], c, bb) for g, bb in zip(groups, b) for c in g[3]]
+            rt = np.array([f * 100 + c + bb for f, c, bb in lanes], np.float32)
+            return rt, -rt, np.zeros(len(lanes), np.uint64)
+    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0: FakePlan(dev))
+    nf = 4
+    feed = engine.FoldFeed(np.zeros(3, np.uint32), np.zeros(3, np.uint32), nf)
+    groups = [(f, a, (lambda f=f: 0.5 * f), [1.0, 2.0, 3.0]) for a in (1.0, 2.0) for f in (3, 1, 0, 2)]
+    want = np.array([f * 100 + c + 0.5 * f for f, _, _, pens in groups for c in pens], np.float32)
+
+    def produce():
+        for f in range(nf):
+            feed.put(f, np.zeros(3, np.uint32), np.zeros(3, np.uint32))
+    th = threading.Thread(target=produce)
+    th.start()
+    rt, re, _ = engine.run_groups("NMN", feed, None, groups, devices=[0])
+    th.join()
+    assert np.array_equal(rt, want)
+    assert log[0] == ("begin", nf)
+    assert [e[1] for e in log if e[0] == "fold"] == [0, 1, 2, 3]
+    passes = [e[1] for e in log if e[0] == "pass"]
+    assert [max(p) for p in passes] == sorted(max(p) for p in passes)
+    bad = engine.FoldFeed(np.zeros(3, np.uint32), np.zeros(3, np.uint32), nf)
+    bad.put(0, np.zeros(3, np.uint32), np.zeros(3, np.uint32))
+    bad.fail(ValueError("split failed"))
+    with pytest.raises(RuntimeError):
+        engine.run_groups("NMN", bad, None, groups, devices=[0])
