@@ -110,11 +110,12 @@ def prepare(gen_pat, seed=1, alphas=ALPHAS, penalties=PENALTIES, nfolds=NFOLDS):
     msum = Mk.sum(axis=0, dtype=np.uint64)
     usum = Uk.sum(axis=0, dtype=np.uint64)
     mtr, utr = msum.sum() - msum, usum.sum() - usum
+    from kmerpapa_amd.shard import fold_order
     groups = []
     for a in alphas:
         my = mtr / (mtr + utr)
         betas = (a * (1.0 - my)) / my
-        for f in range(nfolds):
+        for f in fold_order(nfolds):  # the CV driver's group order (fold 0 last)
             groups.append((f, a, float(betas[f]), list(penalties)))
     return {"Mk": Mk, "Uk": Uk, "groups": groups, "itype": itype, "t_fold_s": t_fold, "contexts": list(table),
             "ctx": table, "Mf": Mf, "Uf": Uf, "total": total, "gen_pat": gen_pat, "alphas": list(alphas),
@@ -152,8 +153,8 @@ def cpu_baseline(prep):
     Uf = prep["Uf"][keep]
     nf = prep["nfolds"]
     bits = 8 * np.dtype(prep["itype"]).itemsize
-    tasks = [(g[1], [prep["groups"][a_i * nf + f][2] for f in range(nf)], c)
-             for a_i, g in enumerate(prep["groups"][::nf]) for c in g[3]]
+    beta = {(g[1], g[0]): g[2] for g in prep["groups"]}
+    tasks = [(a, [beta[(a, f)] for f in range(nf)], c) for a in prep["alphas"] for c in prep["penalties"]]
     O.lib()
 
     def one(task):

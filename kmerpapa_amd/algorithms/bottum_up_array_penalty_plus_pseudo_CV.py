@@ -22,6 +22,7 @@ from .. import engine
 from ..CV_tools import all_counts, fold_stream, fold_tables
 from ..pattern_utils import code, generality, pattern_level, perm_code
 from ..score_utils import get_betas
+from ..shard import fold_order
 
 
 def _itype(nmut, nunmut):
@@ -71,7 +72,7 @@ def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, ity
             # the GPUs' lattice tables and lane buffers are set up while the host draws the
             # fold split (the native split releases the GIL); only lane counts matter here
             shape = [(f, a, 1.0, list(penalties[c0:c0 + engine.MAX_GROUP_LANES]))
-                     for a in alphas for f in range(nfolds) for c0 in range(0, nc, engine.MAX_GROUP_LANES)]
+                     for a in alphas for f in fold_order(nfolds) for c0 in range(0, nc, engine.MAX_GROUP_LANES)]
 
             def _prep():
                 try:
@@ -155,7 +156,7 @@ def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, ity
 
         groups, where = [], []
         for a_i, alpha in enumerate(alphas):
-            for f in range(nfolds):
+            for f in fold_order(nfolds):  # fold 0 last (shard.fold_order); lanes map back by `where`
                 beta = (lambda a_i=a_i, f=f: fold_betas(f)[a_i]) if pipelined else fold_betas(f)[a_i]
                 for c0 in range(0, nc, engine.MAX_GROUP_LANES):
                     chunk = list(penalties[c0:c0 + engine.MAX_GROUP_LANES])

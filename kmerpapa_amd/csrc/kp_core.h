@@ -12,8 +12,9 @@
 //   S[h][lane][Bpad]  f32  train score of cell (h,l) for one lane (lane = one penalty of
 //                          one (alpha, fold) group)
 //   C[h][lane][Bpad]  u8   argmin code: (position << 3) | pair, or KP_SINGLE
-//   K[h][kl][nf+1][2] CT   counts (M, U) of the block's k-mer-low cells kl: slot 0 = all
-//                          data (the sum over folds), slot 1 + f = fold f
+//   K[nf+1][h][kl][2] CT   counts (M, U) of the block's k-mer-low cells kl; slot 0 = all
+//                          data (the sum over folds), slot 1 + f = fold f (slot-major, so a
+//                          fold's table is filled and read with contiguous rows)
 //
 // Tie rule: the reference scans positions 0..k-1, pairs in table order, with a strict
 // "<" starting from +inf, then the single-pattern term with a strict "<" in float64.
@@ -131,20 +132,22 @@ __host__ __device__ inline float kp_single_test(const kp_cnt &c, double logp, do
 // counts
 // ---------------------------------------------------------------------------
 
-// count slots per k-mer-low cell in K: all data + one per fold
+// count slots in K (all data + one per fold) and the elements of one slot
 __host__ __device__ inline uint32_t kp_kslots(const kp_geom &g) { return (uint32_t)g.nf + 1u; }
+__host__ __device__ inline uint64_t kp_kslot_elems(const kp_geom &g) { return g.nblocks * (uint64_t)g.n_kl * 2; }
 
 // counts of one k-mer-low cell of block h for group fold f (f < 0: fit mode)
 template <typename CT>
 __host__ __device__ inline kp_cnt kp_kl_counts(const kp_geom &g, const CT *K, uint64_t h, uint32_t kl, int fold) {
-    const CT *row = K + ((h * g.n_kl + kl) * (uint64_t)kp_kslots(g)) * 2;
+    const CT *row = K + (h * g.n_kl + kl) * 2;
     const uint64_t sm = (uint64_t)row[0], su = (uint64_t)row[1];
     kp_cnt c;
     if (fold < 0) {
         c.mtr = sm; c.utr = su; c.mte = 0; c.ute = 0;
     } else {
-        c.mte = (uint64_t)row[2 + 2 * fold];
-        c.ute = (uint64_t)row[3 + 2 * fold];
+        const CT *fr = row + kp_kslot_elems(g) * (uint64_t)(1 + fold);
+        c.mte = (uint64_t)fr[0];
+        c.ute = (uint64_t)fr[1];
         c.mtr = sm - c.mte;  // get_train (CV :22-24, :56-59): all data minus the fold
         c.utr = su - c.ute;
     }

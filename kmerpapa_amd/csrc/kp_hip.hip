@@ -49,23 +49,24 @@
 
 
 // Fills count slots s0 .. s0+ncol-1 of every block of high level H.  Kin_M/Kin_U are
-// [n_kmers][ncol] (k-mer order): column c goes to slot s0 + c.
+// [n_kmers][ncol] (k-mer order): column c goes to slot s0 + c.  K is slot-major
+// (kp_core.h), so a block's rows of one slot are n_kl contiguous (M, U) pairs.
 template <typename CT>
 __global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables T, uint64_t hbase, int H,
                                                         const CT *__restrict__ Kin_M, const CT *__restrict__ Kin_U,
                                                         uint32_t ncol, uint32_t s0, CT *__restrict__ K) {
     const uint64_t h = T.hlist[hbase + blockIdx.x];
-    const uint32_t S = kp_kslots(g);
-    CT *dst = K + h * (uint64_t)g.n_kl * S * 2;
+    const uint64_t se = kp_kslot_elems(g), row = h * (uint64_t)g.n_kl * 2;
     if (H == 0) {
         // all high digits are nucleotides: the block's k-mer-low cells are k-mers
         uint64_t kbase = 0;
         for (int i = 0; i < g.kh; ++i) kbase += (uint64_t)kp_high_digit(g, h, i) * g.khw[i];
         for (uint32_t e = threadIdx.x; e < g.n_kl * ncol; e += blockDim.x) {
-            const uint32_t kl = e / ncol, c = e % ncol;
+            const uint32_t c = e / g.n_kl, kl = e % g.n_kl;
             const uint64_t src = (kbase + kl) * (uint64_t)ncol + c;
-            dst[2 * (kl * S + s0 + c)] = Kin_M[src];
-            dst[2 * (kl * S + s0 + c) + 1] = Kin_U[src];
+            CT *dst = K + se * (s0 + c) + row + 2 * kl;
+            dst[0] = Kin_M[src];
+            dst[1] = Kin_U[src];
         }
         return;
     }
@@ -81,12 +82,11 @@ __global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables
             break;
         }
     }
-    const CT *a = K + h1 * (uint64_t)g.n_kl * S * 2;
-    const CT *b = K + h2 * (uint64_t)g.n_kl * S * 2;
+    const uint64_t r1 = h1 * (uint64_t)g.n_kl * 2, r2 = h2 * (uint64_t)g.n_kl * 2;
     for (uint32_t e = threadIdx.x; e < g.n_kl * ncol * 2; e += blockDim.x) {
-        const uint32_t kl = e / (2 * ncol), r = e % (2 * ncol);
-        const uint32_t x = kl * S * 2 + 2 * s0 + r;
-        dst[x] = a[x] + b[x];
+        const uint32_t c = e / (2 * g.n_kl), r = e % (2 * g.n_kl);
+        const uint64_t base = se * (s0 + c);
+        K[base + row + r] = K[base + r1 + r] + K[base + r2 + r];
     }
 }
 

@@ -46,6 +46,16 @@ def rank_groups(groups, rank, world):
     return [(f, a, b, pens) for f, a, b, pens, _ in out]
 
 
+def fold_order(nf):
+    """Order of the folds inside each alpha when a CV grid is laid out as groups: fold 0
+    last.  The fold split is drawn fold by fold and fold 0 is ready first (CV driver,
+    CV_tools.fold_stream), so a rank can start once its lowest fold is drawn; with fold 0
+    at the end of every alpha's run, the contiguous lane runs of rank_groups more often
+    hold a fold-0 group (8 ranks over a 5x5x5 grid: every 16-lane share does).  The
+    order of the groups does not change any result (lanes map back by (alpha, fold))."""
+    return list(range(1, nf)) + [0] if nf > 1 else [0]
+
+
 def sharded_run_groups(run_groups, rank, world, all_gather, devices=None):
     """Wrap a ``run_groups(gen_pat, M, U, groups, devices, max_block)`` callable so that
     each rank runs only its chunk and every rank returns the full lane arrays.

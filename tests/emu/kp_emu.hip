@@ -44,26 +44,26 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
     uint32_t Ltot = 0;
     for (int i = 0; i < ngroups; ++i) Ltot += (uint32_t)groups[i].nl;
     g.Ltot = Ltot;
-    const uint64_t KS = kp_kslots(g), per = (uint64_t)g.n_kl * KS * 2;
-    std::vector<CT> K(g.nblocks * per);
-    // counts (kp_counts_kernel): slot 0 = all data (sum of the folds), slot 1 + f = fold f
+    const uint64_t KS = kp_kslots(g), se = kp_kslot_elems(g), per = (uint64_t)g.n_kl * 2;
+    std::vector<CT> K(KS * se);
+    // counts (kp_counts_kernel): slot-major, slot 0 = all data (sum of the folds), slot 1 + f = fold f
     for (int H = 0; H <= hp.hmax; ++H) {
         for (uint64_t q = hp.hoff[H]; q < hp.hoff[H + 1]; ++q) {
             uint64_t h = hp.hlist[q];
-            CT *dst = K.data() + h * per;
             if (H == 0) {
                 uint64_t kbase = 0;
                 for (int i = 0; i < g.kh; ++i) kbase += (uint64_t)kp_high_digit(g, h, i) * g.khw[i];
                 for (uint64_t kl = 0; kl < g.n_kl; ++kl) {
                     CT am = 0, au = 0;
                     for (int f = 0; f < nf; ++f) {
-                        dst[2 * (kl * KS + 1 + f)] = M[(kbase + kl) * nf + f];
-                        dst[2 * (kl * KS + 1 + f) + 1] = U[(kbase + kl) * nf + f];
-                        am += M[(kbase + kl) * nf + f];
-                        au += U[(kbase + kl) * nf + f];
+                        CT *d = K.data() + se * (1 + f) + h * per + 2 * kl;
+                        d[0] = M[(kbase + kl) * nf + f];
+                        d[1] = U[(kbase + kl) * nf + f];
+                        am += d[0];
+                        au += d[1];
                     }
-                    dst[2 * kl * KS] = am;
-                    dst[2 * kl * KS + 1] = au;
+                    K[h * per + 2 * kl] = am;
+                    K[h * per + 2 * kl + 1] = au;
                 }
             } else {
                 uint64_t h1 = h, h2 = h;
@@ -76,7 +76,9 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
                         break;
                     }
                 }
-                for (uint64_t e = 0; e < per; ++e) dst[e] = K[h1 * per + e] + K[h2 * per + e];
+                for (uint64_t s = 0; s < KS; ++s)
+                    for (uint64_t e = 0; e < per; ++e)
+                        K[s * se + h * per + e] = K[s * se + h1 * per + e] + K[s * se + h2 * per + e];
             }
         }
     }

@@ -158,7 +158,7 @@ def test_cv_driver_prepares_devices_during_fold_split():
                        run_groups=run)
     assert res["train"].tobytes() == ref["train"].tobytes() and res["test"].tobytes() == ref["test"].tobytes()
     assert len(seen) == 1 and seen[0][0] == c["gen_pat"]
-    assert seen[0][1] == [(f, a, list(c["penalties"])) for a in c["alphas"] for f in range(c["nfolds"])]
+    assert seen[0][1] == [(f, a, list(c["penalties"])) for a in c["alphas"] for f in shard.fold_order(c["nfolds"])]
 
 
 def test_cv_driver_prepare_errors_surface():
