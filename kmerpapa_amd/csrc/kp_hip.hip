@@ -836,15 +836,20 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         if (u.fold >= p->nf || u.fold < -1) return fail(KP_E_ARG, "fold out of range");
         if (u.fold >= 0 && !p->fold_set[u.fold])
             return fail(KP_E_STATE, "counts of fold " + std::to_string(u.fold) + " are not set (kp_counts_fold)");
-        for (int s = 0; s < u.n_lanes; s += per_wg) {
+        // as few device groups as the workgroup width allows, of near-equal lane counts
+        // (a device group's cost is ~100 ms + ~60 ms per lane at 9-mers, DESIGN.md 5: 7
+        // lanes as 4 + 3 beat 5 + 2)
+        const int nd = (u.n_lanes + per_wg - 1) / per_wg;
+        for (int q = 0, s = 0; q < nd; ++q) {
             kp_group_dev d;
             memset(&d, 0, sizeof(d));
             d.fold = u.fold;
             d.lane0 = (int32_t)lane;
-            d.nl = std::min(per_wg, u.n_lanes - s);
+            d.nl = u.n_lanes / nd + (q < u.n_lanes % nd ? 1 : 0);
             d.alpha = u.alpha;
             d.beta = u.beta;
             for (int j = 0; j < d.nl; ++j) d.pen[j] = u.penalty[s + j];
+            s += d.nl;
             lane += (uint32_t)d.nl;
             dg.push_back(d);
         }

@@ -342,7 +342,8 @@ def test_degenerate_lattices_fit_vs_oracle(eng, gp):
 @pytest.mark.parametrize("per_wg", [1, 2, 3, 4, 6, 7, 8])
 def test_lanes_per_workgroup_vs_oracle(eng, per_wg, monkeypatch):
     """Every lanes-per-workgroup kernel instantiation (KP_LANES_PER_WG; the default is 5)
-    on an 8-penalty group of a small-block 5-mer: all cells equal the oracle's."""
+    on an 8-penalty group (6 or 7 for those widths) of a small-block 5-mer, split into
+    near-equal device groups (8 lanes at width 3: 3 + 3 + 2): all cells equal the oracle's."""
     from kmerpapa_amd.CV_tools import fold_tables
     from kmerpapa_amd.pattern_utils import generality
     from oracle import oracle as O
@@ -359,6 +360,8 @@ def test_lanes_per_workgroup_vs_oracle(eng, per_wg, monkeypatch):
     utr = tot_u.sum() - tot_u
     betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
     pens = [0.5, 1.5, 2.5, 3.5, 4.5, 6.0, 8.0, 11.0]
+    if per_wg in (6, 7):  # groups split into near-equal device groups: 8 lanes would run as 4 + 4
+        pens = pens[:per_wg]
     plan = eng.Plan(eng.get_device(0), gp, 64)
     plan.set_counts(Mk, Uk)
     rt, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
