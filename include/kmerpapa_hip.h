@@ -134,6 +134,10 @@ int kp_fit_leaves(kp_plan *plan, uint32_t lane, uint64_t *leaves, uint64_t cap, 
  * ([npat] each; either pointer may be NULL). */
 int kp_dump_lane(kp_plan *plan, uint32_t lane, float *score, uint8_t *code);
 
+/* Parity check of the device's float64 log (the log of the single-pattern term, CV :61-62 /
+ * Fit :56-57; ROCm's ocml): y[i] = log(x[i]) computed on the context's GPU. */
+int kp_math_log(kp_ctx *ctx, const double *x, double *y, uint64_t n);
+
 /* Host-only (no GPU needed): the cross-validation fold split of CV_tools.py
  * make_all_folds_contextD_patterns :44-57 / sample :5-27 with numpy's legacy
  * RandomState stream.  mt_key[624] / *mt_pos = the MT19937 state of the caller's

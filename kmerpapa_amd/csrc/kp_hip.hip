@@ -327,6 +327,13 @@ __global__ void __launch_bounds__(256) kp_bt_finish(kp_bt_params P) {
     }
 }
 
+// the device's float64 log (ROCm ocml, what the DP's single-pattern term uses) of every
+// element: parity checks against the host C library's log
+__global__ void kp_log_kernel(const double *__restrict__ x, double *__restrict__ y, uint64_t n) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        y[i] = log(x[i]);
+}
+
 // argmin code of every cell of one lane (parity dumps): the sequential decision of kp_core.h
 template <typename CT>
 __global__ void kp_codes_kernel(kp_geom g, kp_dev_tables T, const CT *K, const float *S, kp_group_dev G,
@@ -1131,6 +1138,27 @@ int kp_dump_lane(kp_plan *p, uint32_t lane, float *score, uint8_t *code) {
 }  // extern "C"
 
 extern "C" {
+
+int kp_math_log(kp_ctx *c, const double *x, double *y, uint64_t n) {
+    if (!c || (n && (!x || !y))) return fail(KP_E_ARG, "bad arguments");
+    if (!n) return KP_OK;
+    KP_HIP(hipSetDevice(c->device));
+    double *dx = nullptr, *dy = nullptr;
+    KP_HIP(dmalloc(&dx, n * sizeof(double)));
+    hipError_t e = dmalloc(&dy, n * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) {
+        const unsigned nb = (unsigned)std::min<uint64_t>((n + 255) / 256, 16384);
+        hipLaunchKernelGGL(kp_log_kernel, dim3(nb), dim3(256), 0, c->stream, dx, dy, n);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(y, dy, n * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree(dx);
+    dfree(dy);
+    if (e != hipSuccess) return fail(KP_E_HIP, std::string("kp_math_log: ") + hipGetErrorString(e));
+    return KP_OK;
+}
 
 int kp_fold_sample(uint32_t *mt_key, int32_t *mt_pos, const uint64_t *colors, uint64_t n, uint64_t m,
                    uint64_t *out) {

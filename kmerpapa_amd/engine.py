@@ -61,7 +61,7 @@ class KPPassStats(ctypes.Structure):
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
            "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
            "kp_reserve_lanes", "kp_last_pass_stats", "kp_fit_leaves", "kp_dump_lane", "kp_fold_split",
-           "kp_fold_sample", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free"]
+           "kp_fold_sample", "kp_math_log", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free"]
 
 
 def load():
@@ -102,8 +102,12 @@ def load():
         L.kp_fit_leaves.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u64p]
         L.kp_dump_lane.argtypes = [vp, ctypes.c_uint32, vp, vp]
         L.kp_fold_split.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_int, vp]
+        if hasattr(L, "kp_math_log"):  # (older builds loaded through KMERPAPA_LIB for A/B timing lack it)
+            L.kp_math_log.argtypes = [vp, vp, vp, ctypes.c_uint64]
         L.kp_fold_sample.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_uint64, vp]
         for name in EXPORTS:
+            if not hasattr(L, name):
+                continue
             if name not in ("kp_destroy", "kp_plan_destroy", "kp_last_error", "kp_kmer_table_free"):
                 getattr(L, name).restype = ctypes.c_int
         _lib = L
@@ -232,6 +236,13 @@ class Device:
         fr, tot = ctypes.c_uint64(), ctypes.c_uint64()
         _check(load().kp_device_mem(self._h, ctypes.byref(fr), ctypes.byref(tot)))
         return fr.value, tot.value
+
+    def log(self, x):
+        """float64 log of every element on this GPU (kp_math_log: the DP's device log)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.empty_like(x)
+        _check(load().kp_math_log(self._h, _ptr(x), _ptr(y), ctypes.c_uint64(x.size)))
+        return y
 
     def close(self):
         if self._h:

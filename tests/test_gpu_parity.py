@@ -412,3 +412,25 @@ def test_cli_metrics_line(eng, tmp_path, monkeypatch):
     assert set(rec["phases_s"]) == {"read_input", "pattern_and_zero_fill", "cross_validation", "final_fit", "output"}
     assert rec["gen_pat"] == "NNMNN" and rec["patterns"] > 1
     assert abs(sum(rec["phases_s"].values()) - rec["total_s"]) < 0.05
+
+
+def test_device_log_vs_libm(eng):
+    """The DP's device log (ROCm ocml, through kp_math_log) against the host C library's
+    log, which the oracle and the reference call: within 1 ulp everywhere, equal on nearly
+    every input of the DP's range (p and 1 - p in (0, 1)).  The parity tests proper compare
+    the float32 scores this feeds, bit for bit."""
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.log.argtypes = [ctypes.c_double]
+    libm.log.restype = ctypes.c_double
+    rng = np.random.RandomState(3)
+    n = 100_000
+    x = np.concatenate([rng.uniform(0.0, 1.0, n), 1.0 - rng.uniform(0.0, 0.07, n),
+                        np.exp(rng.uniform(-745.0, 709.0, n)),
+                        np.array([1.0, np.inf, 5e-324, 2.2250738585072014e-308, np.nextafter(1.0, 0)])])
+    got = eng.get_device(0).log(x)
+    want = np.array([libm.log(float(v)) for v in x])
+    ulps = np.abs(got.view(np.int64) - want.view(np.int64))
+    assert ulps.max() <= 1, x[np.argmax(ulps)]
+    assert np.mean(ulps[:2 * n] != 0) < 1e-3  # p, 1 - p: differences are rare
+    assert np.isneginf(eng.get_device(0).log(np.array([0.0]))[0])
