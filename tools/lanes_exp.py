@@ -16,11 +16,12 @@ if len(sys.argv) > 1:  # e.g. "5 3,2": compositions as comma lists
 prep = bench.prepare("NNNNMNNNN")
 plan = engine.get_plan(0, "NNNNMNNNN")
 plan.set_counts(prep["Mk"], prep["Uk"])
-plan.reserve(8)
+plan.reserve(max(8, max(sum(c) for c in comps)))
 g = prep["groups"]
 plan.run([g[0]])  # warm
 for comp in comps:
-    groups = [(g[i][0], g[i][1], g[i][2], g[i][3][:n]) for i, n in enumerate(comp)]
+    # n > 5 lanes: extra penalties 8, 9, ... (the 11-mer grid has 7)
+    groups = [(g[i][0], g[i][1], g[i][2], (list(g[i][3]) + [8.0 + j for j in range(8)])[:n]) for i, n in enumerate(comp)]
     t0 = time.perf_counter()
     plan.run(groups)
     dt = time.perf_counter() - t0
