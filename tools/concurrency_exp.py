@@ -3,10 +3,11 @@
 The low high-level launches of a pass are bound by per-block work (~100 ns per block,
 DESIGN.md 5), the high ones by the gather's bandwidth.  Two independent passes running at
 once on two streams (two kp_ctx on the same device) can mix the two kinds of workgroups.
-This times N passes run one after the other on one stream against the same N passes split
-over two streams (two host threads), and prints units/s for both.
+This times N passes run one after the other on one stream, then two streams running N
+passes each, the second starting OFFSET_MS later (so that its low levels meet the first
+one's high levels), and reports the steady-state period per pass of each stream.
 
-usage: python tools/concurrency_exp.py GEN_PAT LANES NPASSES
+usage: python tools/concurrency_exp.py GEN_PAT LANES NPASSES [OFFSET_MS ...]
 """
 import os
 import sys
@@ -24,38 +25,49 @@ def main():
     gp = sys.argv[1] if len(sys.argv) > 1 else "NNNNMNNN"
     lanes = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     n = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    offsets = [float(x) for x in sys.argv[4:]] or [0.0]
     prep = bench.prepare(gp)
-    groups = [(f, a, b, pens[:lanes]) for f, a, b, pens in prep["groups"]][:n]
+    groups = [(f, a, b, pens[:lanes]) for f, a, b, pens in prep["groups"]]
+    groups = (groups * (1 + 2 * n // len(groups)))[:2 * n]
     devs = [engine.Device(0), engine.Device(0)]
     plans = [engine.Plan(d, gp) for d in devs]
     for p in plans:
         p.reserve(lanes)
         p.set_counts(prep["Mk"], prep["Uk"])
         p.run([groups[0]])  # warm-up
-    units = plans[0].info["npat"] * lanes * len(groups)
+    per_pass_units = plans[0].info["npat"] * lanes
 
     t0 = time.perf_counter()
-    single = [plans[0].run([g]) for g in groups]
-    t_single = time.perf_counter() - t0
+    ref = [plans[0].run([g]) for g in groups[:n]]
+    t_single = (time.perf_counter() - t0) / n
+    print({"gen_pat": gp, "lanes": lanes, "single_ms_per_pass": round(t_single * 1e3, 2),
+           "units_per_s": per_pass_units / t_single}, flush=True)
 
-    out = [None, None]
+    for off in offsets:
+        stamps = [[], []]
+        out = [[], []]
 
-    def work(i):
-        out[i] = [plans[i].run([g]) for g in groups[i::2]]
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=work, args=(i,)) for i in range(2)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    t_dual = time.perf_counter() - t0
-    same = all(single[2 * j + i][0].tobytes() == out[i][j][0].tobytes()
-               for i in range(2) for j in range(len(out[i])))
-    print({"gen_pat": gp, "lanes": lanes, "passes": len(groups), "single_s": round(t_single, 4),
-           "dual_s": round(t_dual, 4), "single_ms_per_pass": round(t_single / len(groups) * 1e3, 2),
-           "dual_ms_per_pass": round(t_dual / len(groups) * 1e3, 2), "speedup": round(t_single / t_dual, 4),
-           "units_per_s_single": units / t_single, "units_per_s_dual": units / t_dual, "roots_equal": same},
-          flush=True)
+        def work(i):
+            if i == 1 and off > 0:
+                time.sleep(off / 1e3)
+            for g in groups[i * n:(i + 1) * n]:
+                out[i].append(plans[i].run([g]))
+                stamps[i].append(time.perf_counter())
+        ths = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+        t0 = time.perf_counter()
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        # steady state: the passes both streams ran side by side (the first and last pass
+        # of each stream overlap the other stream only partly)
+        per = [(s[-2] - s[0]) / (len(s) - 2) for s in stamps]
+        both = 2 * per_pass_units / max(per)
+        same = out[0][0][0].tobytes() == ref[0][0].tobytes()
+        print({"offset_ms": off, "stream_ms_per_pass": [round(x * 1e3, 2) for x in per],
+               "pair_ms": round(max(per) * 1e3, 2), "units_per_s": both, "vs_single": round(both * t_single /
+                                                                                           per_pass_units, 4),
+               "wall_s": round(time.perf_counter() - t0, 3), "roots_equal": same}, flush=True)
     for p in plans:
         p.close()
     for d in devs:
