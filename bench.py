@@ -176,7 +176,50 @@ def cpu_baseline(prep):
             "single_core_value": units / t1,
             "sample": f"oracle/kp_oracle.c kpo_cv (1 thread per task) on sub-lattice {sub} of the same counts "
                       f"({O.npat(sub)} cells x {nf} folds per (alpha,c) task): {par} concurrent tasks on "
-                      f"{par} host cores in {tn:.1f} s; 1 task alone on 1 core in {t1:.1f} s"}
+                      f"{par} host cores in {tn:.1f} s; 1 task alone on 1 core in {t1:.1f} s",
+            "python": python_baseline(prep, tasks, par)}
+
+
+def python_baseline(prep, tasks, par):
+    """The reference-equivalent pure-Python path (oracle/pyref.py: the reference's CV pass
+    as plain Python, what it runs without numba) on a smaller sample of the same counts --
+    the four outermost ambiguous positions fixed to 'A' (151,875 cells for the 9-mer) --
+    one (alpha, c) task per host core, each in its own Python process (the README's
+    one-process-per-grid-point fan-out)."""
+    import subprocess
+    import tempfile
+    from oracle import oracle as O
+    gp = prep["gen_pat"]
+    amb = [i for i, x in enumerate(gp) if x != "A"]
+    fixed = set(amb[:2] + amb[-2:])
+    sub = "".join("A" if i in fixed else x for i, x in enumerate(gp))
+    keep = [j for j, c in enumerate(prep["contexts"]) if all(c[i] == "A" for i in fixed)]
+    ctxs = [prep["contexts"][i] for i in keep]
+    nf = prep["nfolds"]
+    M = O._scatter(sub, ctxs, prep["Mf"][keep], nf)
+    U = O._scatter(sub, ctxs, prep["Uf"][keep], nf)
+    bits = 8 * np.dtype(prep["itype"]).itemsize
+    with tempfile.TemporaryDirectory() as tmp:
+        paths = []
+        for i in range(par):
+            a, betas, c = tasks[i % len(tasks)]
+            paths.append(os.path.join(tmp, f"t{i}.npz"))
+            np.savez(paths[-1], gen_pat=sub, M=M, U=U, alpha=a, betas=np.array(betas), penalty=c, itype_bits=bits)
+        t0 = time.time()
+        procs = [subprocess.Popen([sys.executable, "-m", "oracle.pyref", p], cwd=ROOT, stdout=subprocess.PIPE,
+                                  text=True) for p in paths]
+        outs = [pr.communicate()[0] for pr in procs]
+        tn = time.time() - t0
+        if any(pr.returncode for pr in procs):
+            raise RuntimeError("pure-Python baseline task failed")
+    secs = [float(o.split()[-1]) for o in outs]
+    units = O.npat(sub) * nf
+    return {"value": units * par / tn, "unit": "cells*folds*(alpha,c)/s", "cores": par,
+            "kind": "reference-equivalent pure Python (oracle/pyref.py)",
+            "single_core_value": units / (sum(secs) / len(secs)),
+            "sample": f"oracle/pyref.py cv_pass on sub-lattice {sub} of the same counts ({O.npat(sub)} cells x "
+                      f"{nf} folds per (alpha,c) task): {par} processes on {par} host cores in {tn:.1f} s "
+                      f"(per task {min(secs):.1f}-{max(secs):.1f} s)"}
 
 
 def committed_traffic(gen_pat, n_lanes, kernel_tag):

@@ -44,3 +44,14 @@ def test_pass_cap_is_largest_group_if_it_fits():
 
 def test_host_cores_positive():
     assert bench.host_cores() >= 1
+
+
+def test_python_baseline_runs_pyref_processes():
+    """The pure-Python baseline leg: one oracle/pyref.py process per core on the sample
+    lattice (the four outermost ambiguous positions fixed), its rate reported."""
+    prep = bench.prepare("NNMNNN", alphas=[0.5, 1.0], penalties=[3.0], nfolds=2)
+    beta = {(g[1], g[0]): g[2] for g in prep["groups"]}
+    tasks = [(a, [beta[(a, f)] for f in range(2)], c) for a in prep["alphas"] for c in prep["penalties"]]
+    r = bench.python_baseline(prep, tasks, 2)
+    assert r["cores"] == 2 and r["value"] > 0 and r["single_core_value"] > 0
+    assert "AAMNAA" in r["sample"]
