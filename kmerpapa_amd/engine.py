@@ -498,22 +498,25 @@ _plans = {}
 _cache_lock = threading.Lock()
 
 
-def get_device(dev):
+def get_device(dev, replica=0):
+    """The library context of GPU ``dev``; ``replica`` > 0 = another context (its own HIP
+    stream) on the same GPU, for a device list that names one GPU more than once."""
     with _cache_lock:
-        if dev not in _devices:
-            _devices[dev] = Device(dev)
-        return _devices[dev]
+        if (dev, replica) not in _devices:
+            _devices[(dev, replica)] = Device(dev)
+        return _devices[(dev, replica)]
 
 
-def get_plan(dev, gen_pat, max_block=0):
-    key = (dev, gen_pat, max_block)
+def get_plan(dev, gen_pat, max_block=0, replica=0):
+    key = (dev, gen_pat, max_block, replica)
     with _cache_lock:
         plan = _plans.get(key)
     if plan is None:
-        plan = Plan(get_device(dev), gen_pat, max_block)
+        plan = Plan(get_device(dev, replica), gen_pat, max_block)
         with _cache_lock:
-            # one resident lattice per device: drop other patterns' buffers first
-            for other in [k for k in _plans if k[0] == dev and k != key]:
+            # one resident lattice per device: drop other patterns' buffers first (replicas
+            # of the same lattice stay)
+            for other in [k for k in _plans if k[0] == dev and k[1:3] != key[1:3]]:
                 _plans.pop(other).close()
             _plans[key] = plan
     return plan
@@ -549,20 +552,32 @@ def _device_shares(groups, devices):
     return [rank_groups(groups, slot, len(devices)) for slot in range(len(devices))]
 
 
+def _replicas(devices):
+    """Replica index of every slot: how often its GPU was named before (0 for a list of
+    distinct GPUs).  A GPU named twice gets two contexts and two host threads: that runs
+    the multi-GPU path on one GPU (a rehearsal; the slots share its HBM and bandwidth)."""
+    seen = {}
+    out = []
+    for d in devices:
+        out.append(seen.get(d, 0))
+        seen[d] = out[-1] + 1
+    return out
+
+
 def prepare_groups(gen_pat, groups, devices=None, max_block=0):
     """Everything ``run_groups`` needs before the counts exist: each GPU's plan (lattice
     tables uploaded) and one allocation for its largest pass.  Only the lane counts of
     ``groups`` matter (folds, alphas and betas may be placeholders), so a caller can run
     this while the host draws the fold split (CV_tools.fold_tables drops the GIL)."""
-    devices = list(dict.fromkeys(devices if devices is not None else visible_devices()[:1]))
+    devices = list(devices if devices is not None else visible_devices()[:1])
 
-    def prep(dev, chunk):
+    def prep(dev, rep, chunk):
         if chunk:
-            plan = get_plan(dev, gen_pat, max_block)
+            plan = get_plan(dev, gen_pat, max_block, replica=rep)
             passes = pack_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
             plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
-    threads = [threading.Thread(target=prep, args=(dev, chunk))
-               for dev, chunk in zip(devices, _device_shares(groups, devices))]
+    threads = [threading.Thread(target=prep, args=(dev, rep, chunk))
+               for dev, rep, chunk in zip(devices, _replicas(devices), _device_shares(groups, devices))]
     for th in threads:
         th.start()
     for th in threads:
@@ -582,7 +597,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     ``(root_train, root_test, n_leaves)`` arrays over all lanes, group-major.
     """
     devices = list(devices) if devices is not None else visible_devices()[:1]
-    devices = list(dict.fromkeys(devices))  # one host thread per GPU: a device's plan is not shared
+    reps = _replicas(devices)  # one host thread and one context per slot: a plan is never shared
     if not devices:
         raise KPError(-3, "no GPU visible")
     nd = len(devices)
@@ -596,7 +611,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
         try:
             outs = []
             if chunk:
-                plan = get_plan(dev, gen_pat, max_block)
+                plan = get_plan(dev, gen_pat, max_block, replica=reps[slot])
                 if feed is not None:
                     plan.counts_begin(feed.M_all, feed.U_all, feed.nf)
                 else:

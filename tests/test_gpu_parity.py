@@ -108,6 +108,36 @@ def test_grid5_roots_per_fold(eng):
         assert np.array_equal(res["betas"][0, a_i], np.array(ps["betas"]))
 
 
+def test_grid5_multi_device_path_on_one_gpu(eng, monkeypatch):
+    """The single-process multi-GPU path (engine.run_groups: lane-granular slots, one host
+    thread, context and HIP stream per slot, fold-by-fold count upload) run on the one GPU
+    of the box by naming it 2 and 3 times: per-fold roots and the CVfile equal the
+    reference's (config 2)."""
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    g = golden_json("grid5.json")
+    ctx, gp, nm, nu = context_table(5)
+    for devs in ([0, 0], [0, 0, 0]):
+        res = cvm.cv_roots(gp, ctx, g["alphas"], g["penalties"], 5, 1, 1, np.uint32, devices=devs)
+        for ps in g["passes"]:
+            a_i = g["alphas"].index(ps["alpha"])
+            p_i = g["penalties"].index(ps["penalty"])
+            assert bits_equal(res["test"][0, a_i, p_i], np.array(ps["root_test"], np.float32)), devs
+            assert bits_equal(res["train"][0, a_i, p_i], np.array(ps["root_train"], np.float32)), devs
+    monkeypatch.setenv("KMERPAPA_DEVICES", "0,0")
+    buf = io.StringIO()
+
+    class A:
+        nfolds = 5
+        iterations = 1
+        seed = 1
+        verbosity = 0
+        CVfile = buf
+    best = cvm.pattern_partition_bottom_up(gp, ctx, g["alphas"], A, nm, nu, g["penalties"])
+    assert buf.getvalue() == g["cvfile"]
+    assert [best[0], best[1], best[2]] == g["best"]
+    eng.release_all()  # the replicas' buffers
+
+
 def test_iterations_carry_over(eng):
     """--iterations 2 reproduces the reference's fold totals (its carry-over of the previous
     iteration's aggregated rows, CV :134-137), roots and CVfile (5-mer, tests/golden/iter5.json)."""

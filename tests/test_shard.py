@@ -123,7 +123,7 @@ def test_engine_run_groups_lane_granular_over_devices(monkeypatch):
                 ran.setdefault(ln, []).append(self.dev)
             rt = np.array([f * 1000 + a * 10 + c for f, a, c in lanes], np.float32)
             return rt, -rt, np.arange(len(lanes), dtype=np.uint64)
-    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0: FakePlan(dev))
+    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0, replica=0: FakePlan(dev))
     groups = [(f, a, 0.1, [3.0, 4.0, 5.0, 6.0, 7.0]) for a in (0.5, 1.0, 2.0, 5.0, 10.0) for f in range(5)]
     want = np.array([f * 1000 + a * 10 + c for f, a, _, pens in groups for c in pens], np.float32)
     for devs in ([0], [0, 1], [0, 1, 2], [3, 2, 1, 0, 4, 5, 6, 7]):
@@ -239,7 +239,7 @@ def test_engine_run_groups_fold_feed_order(monkeypatch):
             lanes = [(g[0], c, bb) for g, bb in zip(groups, b) for c in g[3]]
             rt = np.array([f * 100 + c + bb for f, c, bb in lanes], np.float32)
             return rt, -rt, np.zeros(len(lanes), np.uint64)
-    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0: FakePlan(dev))
+    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0, replica=0: FakePlan(dev))
     nf = 4
     feed = engine.FoldFeed(np.zeros(3, np.uint32), np.zeros(3, np.uint32), nf)
     groups = [(f, a, (lambda f=f: 0.5 * f), [1.0, 2.0, 3.0]) for a in (1.0, 2.0) for f in (3, 1, 0, 2)]
@@ -262,3 +262,39 @@ def test_engine_run_groups_fold_feed_order(monkeypatch):
     bad.fail(ValueError("split failed"))
     with pytest.raises(RuntimeError):
         engine.run_groups("NMN", bad, None, groups, devices=[0])
+
+
+def test_engine_run_groups_gpu_named_twice(monkeypatch):
+    """A device list naming a GPU more than once (KMERPAPA_DEVICES=0,0: the multi-GPU path
+    rehearsed on one GPU) gives every slot its own plan replica and host thread; lanes and
+    results are as for distinct GPUs."""
+    from kmerpapa_amd import engine
+    made = []
+
+    class FakePlan:
+        def __init__(self, dev, rep):
+            self.key = (dev, rep)
+            made.append(self.key)
+
+        def set_counts(self, M, U):
+            pass
+
+        def lanes_that_fit(self):
+            return 5
+
+        def reserve(self, lanes):
+            pass
+
+        def run(self, groups):
+            lanes = [(g[0], g[1], c) for g in groups for c in g[3]]
+            rt = np.array([f * 1000 + a * 10 + c for f, a, c in lanes], np.float32)
+            return rt, -rt, np.zeros(len(lanes), np.uint64)
+    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0, replica=0: FakePlan(dev, replica))
+    groups = [(f, a, 0.1, [3.0, 4.0, 5.0]) for a in (0.5, 1.0) for f in range(3)]
+    want = np.array([f * 1000 + a * 10 + c for f, a, _, pens in groups for c in pens], np.float32)
+    for devs in ([0, 0], [1, 0, 1, 1]):
+        made.clear()
+        rt, _, _ = engine.run_groups("NMN", None, None, groups, devices=devs)
+        assert np.array_equal(rt, want)
+        assert sorted(made) == sorted(zip(devs, engine._replicas(devs)))
+    assert engine._replicas([1, 0, 1, 1]) == [0, 0, 1, 2]
