@@ -466,3 +466,42 @@ def test_device_log_vs_libm(eng):
     assert ulps.max() <= 1, x[np.argmax(ulps)]
     assert np.mean(ulps[:2 * n] != 0) < 0.1  # p, 1 - p: last-bit differences on ~4 %
     assert np.isneginf(eng.get_device(0).log(np.array([0.0]))[0])
+
+
+def test_uint64_counts_multilevel_vs_oracle(eng):
+    """Counts whose total exceeds 2^32 - 1 take the reference's uint64 itype (CV :94-97):
+    the 64-bit count tables and kernels (their larger LDS tables put 4 lanes in a workgroup
+    instead of 5) on a 2.3e6-cell lattice with four high levels, 2 folds x 5 penalties:
+    every cell's float32 score and every root, bit for bit against the 64-bit oracle."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality, matches
+    from oracle import oracle as O
+    gp = "NNNMNN"
+    rng = np.random.RandomState(17)
+    ctx = {}
+    for kmer in matches(gp):
+        bg = int(rng.randint(1_000_000, 4_000_000))
+        ctx[kmer] = (int(rng.binomial(bg, 2e-4)), bg)
+    assert sum(m + u for m, u in ctx.values()) > 2**32
+    nf = 2
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(2), np.uint64)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint64)
+    alpha = 0.7
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr = tot_m.sum() - tot_m
+    utr = tot_u.sum() - tot_u
+    betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+    pens = [1.0, 3.0, 5.0, 7.0, 9.0]
+    plan = eng.Plan(eng.get_device(0), gp, 0)
+    assert plan.info["high_levels"] > 3
+    plan.set_counts(Mk, Uk)
+    rt, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
+    for pi, c in enumerate(pens):
+        ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 64)
+        for f in range(nf):
+            lane = f * len(pens) + pi
+            score, _ = plan.dump_lane(lane)
+            assert bits_equal(score, ref["score"][:, f]), (c, f)
+            assert bits_equal(rt[lane], ref["root_train"][f]) and bits_equal(re[lane], ref["root_test"][f])
+    plan.close()
