@@ -374,13 +374,15 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
 // Entries are (M, U) pairs of CT.  tid/nth = this thread and the thread count; sync()
 // separates the steps (a workgroup barrier on the GPU, nothing on the host).
 // ---------------------------------------------------------------------------
+// pre (optional): this thread's first row (k-mer-low cell tid), loaded by the caller ahead
+// of time so the load's latency overlaps other work.
 template <typename CT, typename LM, typename SyncFn>
 __host__ __device__ inline void kp_build_count_table(const kp_geom &g, const CT *K, uint64_t h, int fold, LM lm,
                                                      CT *bufA, CT *bufB, CT *ptab, uint32_t tid, uint32_t nth,
-                                                     SyncFn sync) {
+                                                     SyncFn sync, const kp_cnt *pre = nullptr) {
     CT *out0 = (g.t == 1) ? ptab : bufA;
     for (uint32_t kl = tid; kl < g.n_kl; kl += nth) {
-        const kp_cnt c = kp_kl_counts<CT>(g, K, h, kl, fold);
+        const kp_cnt c = (pre && kl == tid) ? *pre : kp_kl_counts<CT>(g, K, h, kl, fold);
         out0[2 * kl] = (CT)c.mtr;
         out0[2 * kl + 1] = (CT)c.utr;
     }

@@ -24,6 +24,7 @@ struct kp_dev_tables {
     const uint32_t *hlist;
     const kp_lowdesc *ldesc;
     const uint64_t *hdig;
+    const uint64_t *hnp;
     const uint8_t *lowmask;
     const uint4 *lpairs;  // low split-pair lists in 4-pair chunks (kp_plan.h lpairs)
 };
@@ -225,14 +226,29 @@ kp_dp_kernel(kp_dp_params P) {
 #endif
 
     const CT *K = reinterpret_cast<const CT *>(P.K);
-    // the block's high split pairs, scan order (kp_high_pairs): digits come packed from the
-    // plan (no 64-bit division), counts per position are uniform loads, and wave 0 writes
-    // one pair per lane
+    // this thread's k-mer-low count row (the count table's first step), loaded before the
+    // high-pair setup below so that the two latencies overlap (unconditional raw loads from
+    // valid rows -- a branch would make the compiler wait for them at its join -- and the
+    // subtraction after the setup)
+    CT kraw[4];
+    {
+        const uint32_t kl = threadIdx.x < g.n_kl ? threadIdx.x : 0u;
+        const CT *row = K + (h * g.n_kl + kl) * 2;
+        const CT *fr = row + kp_kslot_elems(g) * (uint64_t)(fold >= 0 ? 1 + fold : 0);
+        kraw[0] = row[0];
+        kraw[1] = row[1];
+        kraw[2] = fr[0];
+        kraw[3] = fr[1];
+    }
+    // the block's high split pairs, scan order (kp_high_pairs): digits and pair counts per
+    // high position come packed from the plan (no 64-bit division, no table lookups: the
+    // only dependent loads are the pair digits), and wave 0 writes one pair per lane
     const uint64_t hd = P.T.hdig[P.hbase + widx];
+    const uint64_t hn = P.T.hnp[P.hbase + widx];
     int np = 0, nnt = 0;
     if (!KP_SKIP(P, 1))
         for (int i = 0; i < g.kh; ++i) {
-            const int npi = P.T.tabs[g.t + i].np[(hd >> (4 * i)) & 15u];
+            const int npi = (int)(hn >> (3 * i)) & 7;
             np += npi;
             if ((P.ntmask >> i) & 1u) nnt += npi;
         }
@@ -244,7 +260,7 @@ kp_dp_kernel(kp_dp_params P) {
         uint32_t d = 0;
         for (; i < g.kh; ++i) {
             d = (uint32_t)(hd >> (4 * i)) & 15u;
-            const int npi = P.T.tabs[g.t + i].np[d];
+            const int npi = (int)(hn >> (3 * i)) & 7;
             if (rem < npi) break;
             rem -= npi;
             if ((P.ntmask >> i) & 1u) before_nt += npi; else before_t += npi;
@@ -259,9 +275,12 @@ kp_dp_kernel(kp_dp_params P) {
     __syncthreads();  // lm is read by every thread below
 
     // ---- separable count tables (train counts of the group fold), kp_core.h ----
+    // (kp_kl_counts of the preloaded row: train = all data - fold, CV :22-24)
+    const uint64_t kte_m = fold >= 0 ? (uint64_t)kraw[2] : 0, kte_u = fold >= 0 ? (uint64_t)kraw[3] : 0;
+    const kp_cnt kpre = {(uint64_t)kraw[0] - kte_m, (uint64_t)kraw[1] - kte_u, kte_m, kte_u};
     kp_build_count_table<CT>(g, K, h, fold, lm, reinterpret_cast<CT *>(smem),
                              reinterpret_cast<CT *>(smem) + (size_t)P.pscratch_entries * 2, ptab, threadIdx.x,
-                             blockDim.x, [] { __syncthreads(); });
+                             blockDim.x, [] { __syncthreads(); }, &kpre);
     __syncthreads();
     KP_STAMP(0);
 

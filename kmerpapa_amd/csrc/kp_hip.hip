@@ -386,6 +386,7 @@ struct kp_plan {
     uint32_t *d_hlist = nullptr;
     kp_lowdesc *d_ldesc = nullptr;
     uint64_t *d_hdig = nullptr;
+    uint64_t *d_hnp = nullptr;
     uint8_t *d_lowmask = nullptr;
     uint32_t *d_lpairs = nullptr;
     // counts
@@ -426,6 +427,7 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     T.hlist = p->d_hlist;
     T.ldesc = p->d_ldesc;
     T.hdig = p->d_hdig;
+    T.hnp = p->d_hnp;
     T.lowmask = p->d_lowmask;
     T.lpairs = reinterpret_cast<const uint4 *>(p->d_lpairs);
     return T;
@@ -519,7 +521,7 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
         (rc = upload(&p->d_loff, p->hp.loff)) || (rc = upload(&p->d_klofs, p->hp.klofs)) ||
         (rc = upload(&p->d_kllist, p->hp.kllist)) || (rc = upload(&p->d_hlist, p->hp.hlist)) ||
         (rc = upload(&p->d_ldesc, p->hp.ldesc)) ||
-        (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_lowmask, p->hp.lowmask)) ||
+        (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_hnp, p->hp.hnp)) || (rc = upload(&p->d_lowmask, p->hp.lowmask)) ||
         (rc = upload(&p->d_lpairs, p->hp.lpairs))) {
         kp_plan_destroy(p);
         return rc;
@@ -533,7 +535,7 @@ void kp_plan_destroy(kp_plan *p) {
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
     free_scores(p);
     void *bufs[] = {p->d_tabs,    p->d_lowinfo, p->d_loff,   p->d_klofs,   p->d_kllist, p->d_hlist, p->d_ldesc,
-                    p->d_hdig,    p->d_lowmask, p->d_lpairs, p->d_K,      p->d_nodes, p->d_groups,
+                    p->d_hdig,    p->d_hnp,     p->d_lowmask, p->d_lpairs, p->d_K,      p->d_nodes, p->d_groups,
                     p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
                     p->d_leaves};
     for (void *b : bufs) dfree(b);

@@ -55,6 +55,7 @@ struct host_plan {
     std::vector<uint16_t> kllist;      // k-mer-low cells matching each low cell
     std::vector<uint32_t> hlist;       // [nblocks] blocks sorted by high level
     std::vector<uint64_t> hdig;        // [nblocks] their high digits, 4 bits per high position
+    std::vector<uint64_t> hnp;         // [nblocks] their split pairs per high position, 3 bits each
     std::vector<uint64_t> hoff;        // [hmax + 2]
     std::vector<int> perm;             // high positions of the block order, fastest first
     uint32_t kh_nuc_weight = 0;
@@ -409,6 +410,12 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
             for (int i = 0; i < g.kh; ++i) w |= (uint64_t)kp_high_digit(g, h, i) << (4 * i);
             P.hdig[q] = w;
         }
+    }
+    P.hnp.resize(g.nblocks);
+    for (uint64_t q = 0; q < g.nblocks; ++q) {
+        uint64_t n = 0;
+        for (int i = 0; i < g.kh; ++i) n |= (uint64_t)P.tabs[t + i].np[(P.hdig[q] >> (4 * i)) & 15u] << (3 * i);
+        P.hnp[q] = n;
     }
     // split pairs per position: sum over digits of np, times the other radices
     for (int i = 0; i < k; ++i) {
