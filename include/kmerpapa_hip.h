@@ -138,6 +138,11 @@ int kp_dump_lane(kp_plan *plan, uint32_t lane, float *score, uint8_t *code);
  * Fit :56-57; ROCm's ocml): y[i] = log(x[i]) computed on the context's GPU. */
 int kp_math_log(kp_ctx *ctx, const double *x, double *y, uint64_t n);
 
+/* Parity check of the C library's log / log1p as restated for the GPU (kp_libm.h: the
+ * sweep's exact fallback, the backtrack and the k-mer terms): fn 1 = log, 2 = log1p
+ * (fn 0 = the device's own log, as kp_math_log), computed on the context's GPU. */
+int kp_math_libm(kp_ctx *ctx, const double *x, double *y, uint64_t n, int fn);
+
 /* Host-only (no GPU needed): the cross-validation fold split of CV_tools.py
  * make_all_folds_contextD_patterns :44-57 / sample :5-27 with numpy's legacy
  * RandomState stream.  mt_key[624] / *mt_pos = the MT19937 state of the caller's

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kp_libm.h"
+
 #define KP_MAXK 16          // pattern length limit (15^16 cells is far beyond any HBM)
 #define KP_MAXT 8           // low positions per block
 #define KP_GROUP_LANES 8    // penalties per (alpha, fold) group
@@ -90,12 +92,13 @@ struct kp_lowdesc {
 // scoring arithmetic (float64, order of operations as in the reference)
 // ---------------------------------------------------------------------------
 
-// scipy.special.xlogy / xlog1py: 0 when x == 0 and y is not NaN
+// scipy.special.xlogy / xlog1py: 0 when x == 0 and y is not NaN; the logs are the C
+// library's (kp_libm.h), as scipy's are
 __host__ __device__ inline double kp_xlogy(double x, double y) {
-    return (x == 0.0 && y == y) ? 0.0 : x * log(y);  // y == y: not NaN
+    return (x == 0.0 && y == y) ? 0.0 : x * kp_libm_log(y);  // y == y: not NaN
 }
 __host__ __device__ inline double kp_xlog1py(double x, double y) {
-    return (x == 0.0 && y == y) ? 0.0 : x * log1p(y);
+    return (x == 0.0 && y == y) ? 0.0 : x * kp_libm_log1p(y);
 }
 
 // p = (M_tr + a) / (M_tr + U_tr + a + beta), summed left to right (CV :60, Fit :56)
@@ -211,6 +214,7 @@ struct kp_single_ctx {
     bool kmer;      // level-0 cell: reference uses the xlogy formula and no splits
     double logp, log1mp;
     kp_cnt c;
+    bool exact;     // every cell takes the C library's logs (KP_EXACT_LOGS=1, or !kp_fast_logs_ok)
 };
 
 // ---------------------------------------------------------------------------
@@ -260,16 +264,61 @@ __host__ __device__ inline void kp_pairs_minv(SP st, uint32_t l, uint32_t cg, ui
         for (int j = 0; j < W; ++j) lmin[j] = fminf(lmin[j], va[p][j] + vb[p][j]);
 }
 
+// Float32 stores that cannot depend on the last bit of a float64 log.  The sweep takes its
+// logs from the device's own log (ROCm ocml: within 1 ulp of the C library's,
+// test_device_log_vs_libm), cheaper in this kernel than the C library's algorithm.  A
+// single-pattern term s = c + (-2 M) log p + (-2 U) log(1-p) reaches the store only as
+// float32(s) when s < best (otherwise the stored value is best, and then a nearby s rounds
+// to best as well); so the result equals the C library's unless s lies close to a float32
+// rounding midpoint.  Premise (kp_fast_logs_ok): c, alpha, beta >= 0, so every term is >= 0
+// and s is exactly 0 or a float32 normal (the smallest nonzero s is ~ min(beta, 1/total) >>
+// 2^-126).  Then a 2-ulp difference of the two logs moves s by less than 2.5 x 2^-51 |s|
+// through the reference's three float64 operations, i.e. by fewer than 11 units in the last
+// place of s, and the float32 rounding midpoints are the float64 values whose low 29
+// mantissa bits are 2^28.  kp_store_unsafe flags an s whose low 29 bits are within 64
+// units of 2^28 (s = 0 never is); a cell with a flagged lane recomputes its logs with the C
+// library's algorithm (kp_libm_log, out of line) -- about 2.4e-7 of the lanes.  Groups
+// outside the premise take that path for every cell (kp_single_ctx.exact).
+__host__ __device__ inline bool kp_store_unsafe(double s) {
+    const uint32_t lo = (uint32_t)__builtin_bit_cast(uint64_t, s);
+    return ((lo + 64u) & 0x1FFFFF80u) == 0x10000000u;
+}
+
+// the fast path's premise (kp_store_unsafe): penalties, alpha and beta not negative, and
+// beta either 0 or not so small that a single term could fall below float32's normal range
+__host__ __device__ inline bool kp_fast_logs_ok(const double *pen, int n, double alpha, double beta) {
+    bool ok = alpha >= 0.0 && alpha < 1e30 && (beta == 0.0 || (beta >= 1e-30 * (1.0 + alpha) && beta < 1e30));
+    for (int j = 0; j < n; ++j) ok = ok && pen[j] >= 0.0 && pen[j] < 1e30;
+    return ok;
+}
+
 // a cell's final score per lane: min(best split, single term)
 template <int W, typename SP>
-__host__ __device__ inline void kp_cell_store(SP row, const float *lmin, const kp_single_ctx &sc, const double *pen) {
+__host__ __device__ inline void kp_cell_store(SP row, const float *lmin, const kp_single_ctx &sc, const double *pen,
+                                              double alpha, double beta) {
+    float out[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-        float best = lmin[j];
         const double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
-        if (s < (double)best) best = (float)s;  // float64 compare against the float32 store (CV :71)
-        row[j] = best;
+        out[j] = s < (double)lmin[j] ? (float)s : lmin[j];  // float64 compare against the float32 store (CV :71)
     }
+    bool unsafe = sc.exact;
+#pragma unroll
+    for (int j = 0; j < W; ++j)  // (every lane, stored or not: cheaper than telling them apart)
+        unsafe = unsafe || kp_store_unsafe(kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]));
+    if (__builtin_expect(unsafe, 0)) {  // the C library's logs (rare; laid out away from the hot path)
+        const double p = kp_rate(sc.c, alpha, beta);
+        const double lp = kp_libm_log(p), l1p = kp_libm_log(1.0 - p);
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            float best = lmin[j];
+            const double s = kp_single_train(sc.c, lp, l1p, pen[j]);
+            if (s < (double)best) best = (float)s;
+            out[j] = best;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) row[j] = out[j];
 }
 
 // one DP cell for lanes j0 .. j0+W-1 of the NL lanes interleaved in LDS
@@ -282,7 +331,7 @@ __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint3
                                                   const kp_single_ctx &sc, double alpha, double beta,
                                                   const double *pen, uint32_t j0 = 0) {
     SP row = st + l * NL + j0;
-    if (sc.kmer) {  // level 0 (CV :145-151 / Fit :106-114)
+    if (__builtin_expect(sc.kmer, 0)) {  // level 0 (CV :145-151 / Fit :106-114)
 #pragma unroll
         for (int j = 0; j < W; ++j) row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
         return;
@@ -316,7 +365,7 @@ __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint3
             }
         }
     }
-    kp_cell_store<W>(row, lmin, sc, pen);
+    kp_cell_store<W>(row, lmin, sc, pen, alpha, beta);
 }
 
 // min over one 4-pair chunk of a cell's split-pair list (c1 | c2 << 16 per pair, kp_plan.h
@@ -351,7 +400,7 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
                                                 const kp_single_ctx &sc, double alpha, double beta,
                                                 const double *pen, uint32_t j0 = 0) {
     SP row = st + l * NL + j0;
-    if (sc.kmer) {  // level 0 (CV :145-151 / Fit :106-114)
+    if (__builtin_expect(sc.kmer, 0)) {  // level 0 (CV :145-151 / Fit :106-114)
 #pragma unroll
         for (int j = 0; j < W; ++j) row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
         return;
@@ -363,7 +412,7 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
     for (int k = 0; k < KP_PRE_CHUNKS; ++k)
         if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
     for (uint32_t k = KP_PRE_CHUNKS; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
-    kp_cell_store<W>(row, lmin, sc, pen);
+    kp_cell_store<W>(row, lmin, sc, pen, alpha, beta);
 }
 
 // ---------------------------------------------------------------------------
@@ -477,7 +526,7 @@ __host__ __device__ inline float kp_leaf_test_term(const kp_cnt &c, bool kmer, i
     if (fold < 0) return 0.0f;
     if (kmer) return kp_kmer_test(c, alpha, beta);
     const double p = kp_rate(c, alpha, beta);
-    return kp_single_test(c, log(p), log(1.0 - p));
+    return kp_single_test(c, kp_libm_log(p), kp_libm_log(1.0 - p));
 }
 
 // The reference's decision for one cell, recomputed from final child scores: splits in
@@ -508,7 +557,7 @@ __host__ __device__ inline uint32_t kp_cell_decide(const kp_geom &g, const kp_po
         }
     }
     const double p = kp_rate(c, alpha, beta);
-    const double s = kp_single_train(c, log(p), log(1.0 - p), pen);
+    const double s = kp_single_train(c, kp_libm_log(p), kp_libm_log(1.0 - p), pen);
     if (s < (double)best) {
         best = (float)s;
         code = KP_SINGLE;

@@ -46,6 +46,7 @@ struct kp_dp_params {
     int ntstore;    // 1 = score rows stored non-temporally (default; KP_NT_STORE=0 for plain stores)
     uint32_t ntmask;  // high positions whose child rows are loaded non-temporally (bit i = high position i)
     unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
+    int exact;      // 1 = every cell's single term from the C library's logs (KP_EXACT_LOGS=1)
     int dbg;  // -DKP_ABLATION builds only (KP_DEBUG_SKIP, wrong results; always 0 otherwise): 1 = skip gather, 2 = skip level phase,
               // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier
 };
@@ -182,7 +183,10 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
 #ifndef KP_SMALL_WAVES
 #define KP_SMALL_WAVES 6
 #endif
-template <typename CT, int NL>
+// HZ: the build that handles k-mer cells (only high level 0's blocks hold them; their
+// xlogy / xlog1py terms call the C library's logs, kp_libm.h); launches of higher levels
+// may use the build without that code (kp_hip.hip launch_dp)
+template <typename CT, int NL, bool HZ>
 __global__ void __launch_bounds__(KP_DP_MAX_THREADS) __attribute__((amdgpu_waves_per_eu(NL <= 3 ? KP_SMALL_WAVES : 1)))
 kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -211,6 +215,7 @@ kp_dp_kernel(kp_dp_params P) {
     double pen[NL];
 #pragma unroll
     for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
+    const bool exact = P.exact != 0 || !kp_fast_logs_ok(G->pen, G->nl, alpha, beta);
 
     // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | lm[t][16]
     //      (count-table scratch aliases st, which the gather fills afterwards; every carve
@@ -294,7 +299,7 @@ kp_dp_kernel(kp_dp_params P) {
     // ---- levels: low cells inside the block, level by level ----
     // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
     // the next level's descriptors are loaded while the current level computes
-    const bool high_zero = (P.H == 0);
+    const bool high_zero = HZ && P.H == 0;
     const int lmax = KP_SKIP(P, 2) ? -1 : P.lmax;
     const uint4 *desc = reinterpret_cast<const uint4 *>(P.T.ldesc);
     // narrow levels (cells x lanes <= threads, e.g. the block's top levels) split each
@@ -341,6 +346,7 @@ kp_dp_kernel(kp_dp_params P) {
                 for (int c = 0; c < KP_PRE_CHUNKS; ++c)
                     if (4u * c < npairs) pre[c] = lp[c];
                 kp_single_ctx sc;
+                sc.exact = exact;
                 kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
                 sc.kmer = high_zero && lam == 0;
                 sc.c.mte = sc.c.ute = 0;
@@ -370,6 +376,7 @@ kp_dp_kernel(kp_dp_params P) {
                     if (4u * c < npairs) pre[c] = lp[c];
                 // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
                 kp_single_ctx sc;
+                sc.exact = exact;
                 kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
                 sc.kmer = high_zero && lam == 0;
                 sc.c.mte = sc.c.ute = 0;

@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) kp_bt_level(kp_bt_params P) {
             if (fold >= 0) test = kp_kmer_test(c, alpha, beta);
         } else {
             const double pr = kp_rate(c, alpha, beta);
-            const double lp = log(pr), l1p = log(1.0 - pr);
+            const double lp = kp_libm_log(pr), l1p = kp_libm_log(1.0 - pr);  // the C library's (kp_libm.h)
             const double s = kp_single_train(c, lp, l1p, pen);
             value = best;
             if (s < (double)best) {
@@ -327,11 +327,11 @@ __global__ void __launch_bounds__(256) kp_bt_finish(kp_bt_params P) {
     }
 }
 
-// the device's float64 log (ROCm ocml, what the DP's single-pattern term uses) of every
-// element: parity checks against the host C library's log
-__global__ void kp_log_kernel(const double *__restrict__ x, double *__restrict__ y, uint64_t n) {
+// the C library's log (fn 1) or log1p (fn 2) as restated for the device (kp_libm.h), or the
+// device's own log (fn 0)
+__global__ void kp_libm_kernel(const double *__restrict__ x, double *__restrict__ y, uint64_t n, int fn) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        y[i] = log(x[i]);
+        y[i] = fn == 1 ? kp_libm_log(x[i]) : fn == 2 ? kp_libm_log1p(x[i]) : log(x[i]);
 }
 
 // argmin code of every cell of one lane (parity dumps): the sequential decision of kp_core.h
@@ -691,14 +691,23 @@ static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
         ;
 }
 
-template <typename CT, int NL>
-static int launch_dp(kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
+template <typename CT, int NL, bool HZ>
+static int launch_dp_hz(kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
     if (lds > 65536)
-        KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_kernel<CT, NL>),
+        KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_kernel<CT, NL, HZ>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((kp_dp_kernel<CT, NL>), dim3(nb, ngroups), dim3(threads), lds, c->stream, P);
+    hipLaunchKernelGGL((kp_dp_kernel<CT, NL, HZ>), dim3(nb, ngroups), dim3(threads), lds, c->stream, P);
     KP_HIP(hipGetLastError());
     return KP_OK;
+}
+
+// Groups of 1-3 lanes (80 VGPRs at 6 waves per SIMD) run high levels >= 1 without the
+// k-mer code (fewer spills: 1-lane pass 149 -> 144 ms); wider groups keep one kernel for
+// every level (the split build measured slower there: 5 lanes 395 -> 402 ms)
+template <typename CT, int NL>
+static int launch_dp(kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
+    return (P.H == 0 || NL > 3) ? launch_dp_hz<CT, NL, true>(c, P, nb, ngroups, threads, lds)
+                                : launch_dp_hz<CT, NL, false>(c, P, nb, ngroups, threads, lds);
 }
 
 template <typename CT>
@@ -919,6 +928,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     // XCDs): neighbours in the reuse order share their L2; measured -1 %
     P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 8;
     P.lanesplit = getenv("KP_LANE_SPLIT") ? atoi(getenv("KP_LANE_SPLIT")) : 1;
+    // KP_EXACT_LOGS=1: no fast device log at all (same results; exercises the exact path)
+    P.exact = getenv("KP_EXACT_LOGS") ? atoi(getenv("KP_EXACT_LOGS")) : 0;
     P.ntstore = getenv("KP_NT_STORE") ? atoi(getenv("KP_NT_STORE")) : 1;
     // child rows along the KP_NT_SLOW slowest-varying high positions of the block order
     // (default 3) are read non-temporally: under that order they are not re-read while
@@ -1141,8 +1152,10 @@ int kp_dump_lane(kp_plan *p, uint32_t lane, float *score, uint8_t *code) {
 
 extern "C" {
 
-int kp_math_log(kp_ctx *c, const double *x, double *y, uint64_t n) {
-    if (!c || (n && (!x || !y))) return fail(KP_E_ARG, "bad arguments");
+int kp_math_log(kp_ctx *c, const double *x, double *y, uint64_t n) { return kp_math_libm(c, x, y, n, 0); }
+
+int kp_math_libm(kp_ctx *c, const double *x, double *y, uint64_t n, int fn) {
+    if (!c || (n && (!x || !y)) || fn < 0 || fn > 2) return fail(KP_E_ARG, "bad arguments");
     if (!n) return KP_OK;
     KP_HIP(hipSetDevice(c->device));
     double *dx = nullptr, *dy = nullptr;
@@ -1151,14 +1164,14 @@ int kp_math_log(kp_ctx *c, const double *x, double *y, uint64_t n) {
     if (e == hipSuccess) e = hipMemcpyAsync(dx, x, n * sizeof(double), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) {
         const unsigned nb = (unsigned)std::min<uint64_t>((n + 255) / 256, 16384);
-        hipLaunchKernelGGL(kp_log_kernel, dim3(nb), dim3(256), 0, c->stream, dx, dy, n);
+        hipLaunchKernelGGL(kp_libm_kernel, dim3(nb), dim3(256), 0, c->stream, dx, dy, n, fn);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipMemcpyAsync(y, dy, n * sizeof(double), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dfree(dx);
     dfree(dy);
-    if (e != hipSuccess) return fail(KP_E_HIP, std::string("kp_math_log: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return fail(KP_E_HIP, std::string("kp_math_libm: ") + hipGetErrorString(e));
     return KP_OK;
 }
 

@@ -61,7 +61,7 @@ class KPPassStats(ctypes.Structure):
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
            "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
            "kp_reserve_lanes", "kp_last_pass_stats", "kp_fit_leaves", "kp_dump_lane", "kp_fold_split",
-           "kp_fold_sample", "kp_math_log", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free"]
+           "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free"]
 
 
 def load():
@@ -104,6 +104,8 @@ def load():
         L.kp_fold_split.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_int, vp]
         if hasattr(L, "kp_math_log"):  # (older builds loaded through KMERPAPA_LIB for A/B timing lack it)
             L.kp_math_log.argtypes = [vp, vp, vp, ctypes.c_uint64]
+        if hasattr(L, "kp_math_libm"):
+            L.kp_math_libm.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int]
         L.kp_fold_sample.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_uint64, vp]
         for name in EXPORTS:
             if not hasattr(L, name):
@@ -125,7 +127,7 @@ def _ptr(a):
 
 # launch knobs read by kp_hip.hip (every setting gives the same scores; they change timing)
 LAUNCH_KNOBS = ("KP_DP_THREADS", "KP_LANES_PER_WG", "KP_XCD_REMAP", "KP_LANE_SPLIT", "KP_NT_STORE", "KP_NT_SLOW",
-                "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER")
+                "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER", "KP_EXACT_LOGS")
 
 
 def kernel_tag():
@@ -242,6 +244,13 @@ class Device:
         x = np.ascontiguousarray(x, dtype=np.float64)
         y = np.empty_like(x)
         _check(load().kp_math_log(self._h, _ptr(x), _ptr(y), ctypes.c_uint64(x.size)))
+        return y
+
+    def libm(self, x, fn):
+        """The C library's log (fn 1) or log1p (fn 2) as the GPU computes it (kp_math_libm)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        y = np.empty_like(x)
+        _check(load().kp_math_libm(self._h, _ptr(x), _ptr(y), ctypes.c_uint64(x.size), int(fn)))
         return y
 
     def close(self):

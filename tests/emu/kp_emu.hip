@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../kmerpapa_amd/csrc/kp_core.h"
+#include "../../kmerpapa_amd/csrc/kp_libm.h"
 #include "../../kmerpapa_amd/csrc/kp_plan.h"
 
 namespace {
@@ -112,6 +113,7 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
                     for (int qq = hp.loff[lam]; qq < hp.loff[lam + 1]; ++qq) {
                         const kp_lowdesc &D = hp.ldesc[qq];
                         kp_single_ctx sc;
+                        sc.exact = !kp_fast_logs_ok(G.pen, G.nl, G.alpha, G.beta);
                         kp_ptab_counts<CT>(g, hp.lowmask.data(), ptab.data(), D.l, D.info, &sc.c.mtr, &sc.c.utr);
                         sc.c.mte = sc.c.ute = 0;
                         sc.kmer = (H == 0 && lam == 0);
@@ -187,6 +189,11 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
 
 extern "C" {
 const char *emu_last_error(void) { return g_err.c_str(); }
+
+// the C library restatement of kp_libm.h, host build: which = 0 log, 1 log1p
+void emu_libm(const double *x, double *y, uint64_t n, int which) {
+    for (uint64_t i = 0; i < n; ++i) y[i] = which ? kp_libm_log1p(x[i]) : kp_libm_log(x[i]);
+}
 
 // groups: device-group records (fold, lane0, nl, alpha, beta, pen[8]); M/U [n_kmers][nf]
 int emu_run(const char *gp, uint32_t max_block, const void *M, const void *U, int nf, int itype_bytes,

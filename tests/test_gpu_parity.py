@@ -505,3 +505,64 @@ def test_uint64_counts_multilevel_vs_oracle(eng):
             assert bits_equal(score, ref["score"][:, f]), (c, f)
             assert bits_equal(rt[lane], ref["root_train"][f]) and bits_equal(re[lane], ref["root_test"][f])
     plan.close()
+
+
+def test_device_libm_exact(eng):
+    """The C library's log and log1p as restated for the GPU (kp_libm.h: the sweep's exact
+    fallback, the backtrack's single terms, the k-mer cells' xlogy / xlog1py) equal this
+    box's C library bit for bit, on the DP's ranges and across the float64 range."""
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    fns = {}
+    for name in ("log", "log1p"):
+        f = getattr(libm, name)
+        f.argtypes = [ctypes.c_double]
+        f.restype = ctypes.c_double
+        fns[name] = f
+    rng = np.random.RandomState(21)
+    n = 200_000
+    x = np.concatenate([rng.uniform(0.0, 1.0, n), 1.0 - rng.uniform(0.0, 1e-3, n), 1.0 + rng.uniform(-0.07, 0.07, n),
+                        np.exp(rng.uniform(-745.0, 709.0, n)),
+                        np.array([0.0, 1.0, np.inf, np.nan, -1.0, 5e-324, np.nextafter(1.0, 0)])])
+    dev = eng.get_device(0)
+    for fn, name, xs in ((1, "log", x), (2, "log1p", np.concatenate([-x[:2 * n], x[2 * n:]]))):
+        got = dev.libm(xs, fn)
+        want = np.array([fns[name](float(v)) for v in xs])
+        same = (got.view(np.int64) == want.view(np.int64)) | (np.isnan(got) & np.isnan(want))
+        assert same.all(), (name, xs[~same][:5])
+
+
+@pytest.mark.parametrize("seed", [30, 31])
+def test_exact_logs_mode_same_scores(eng, seed, monkeypatch):
+    """KP_EXACT_LOGS=1 (every cell's single term from the C library's logs, no fast device
+    log) gives the same float32 scores as the default guarded fast path and as the oracle:
+    the fallback path itself is right, and the fast path's guard lets nothing through."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    from oracle import oracle as O
+    rng = random.Random(seed)
+    gp, ctx = _random_case(rng, 5)
+    nf = 3
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(seed), np.uint32)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    alpha = 0.5
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr, utr = tot_m.sum() - tot_m, tot_u.sum() - tot_u
+    betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+    pens = [0.0, 3.0, 6.5]
+    groups = [(f, alpha, float(betas[f]), pens) for f in range(nf)]
+    scores = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("KP_EXACT_LOGS", mode)
+        plan = eng.Plan(eng.get_device(0), gp, 64)
+        plan.set_counts(Mk, Uk)
+        rt, re, _ = plan.run(groups)
+        scores[mode] = [plan.dump_lane(ln)[0] for ln in range(nf * len(pens))] + [rt, re]
+        plan.close()
+    for a, b in zip(scores["0"], scores["1"]):
+        assert bits_equal(a, b)
+    for pi, c in enumerate(pens):
+        ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 32)
+        for f in range(nf):
+            assert bits_equal(scores["1"][f * len(pens) + pi], ref["score"][:, f])
