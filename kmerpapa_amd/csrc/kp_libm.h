@@ -62,7 +62,7 @@ __host__ __device__ __attribute__((noinline)) inline double kp_libm_log(double x
     if (top - 0x0010u >= 0x7ff0u - 0x0010u) {  // subnormal, zero, negative, inf or NaN
         if (ix * 2 == 0) return -__builtin_huge_val();
         if (ix == 0x7ff0000000000000ull) return x;
-        if ((top & 0x8000u) || (top & 0x7ff0u) == 0x7ff0u) return __builtin_nan("");
+        if ((top & 0x8000u) || (top & 0x7ff0u) == 0x7ff0u) return (x - x) / (x - x);  // NaN (an input NaN propagates)
         ix = kp_asu64(x * 0x1p52) - (52ull << 52);  // normalise the subnormal
     }
     const uint64_t tmp = ix - 0x3fe6000000000000ull;
@@ -96,9 +96,9 @@ __host__ __device__ __attribute__((noinline)) inline double kp_libm_log1p(double
     int32_t k = 1, hu = 0;
     double f = 0.0, c = 0.0;
     if (hx < 0x3FDA827A) {  // x < 0.41422
-        if (ax >= 0x3ff00000) {  // x <= -1
+        if (ax >= 0x3ff00000) {  // x <= -1 (or a negative NaN)
             if (x == -1.0) return -__builtin_huge_val();
-            return __builtin_nan("");
+            return (x - x) / (x - x);  // NaN (an input NaN propagates)
         }
         if (ax < 0x3e200000) {  // |x| < 2^-29
             if (ax < 0x3c900000) return x;

@@ -521,15 +521,19 @@ def test_device_libm_exact(eng):
         fns[name] = f
     rng = np.random.RandomState(21)
     n = 200_000
+    nans = np.array([0x7ff8000000000000, 0xfff8000000000000, 0x7ff8000000000123], np.uint64).view(np.float64)
     x = np.concatenate([rng.uniform(0.0, 1.0, n), 1.0 - rng.uniform(0.0, 1e-3, n), 1.0 + rng.uniform(-0.07, 0.07, n),
-                        np.exp(rng.uniform(-745.0, 709.0, n)),
-                        np.array([0.0, 1.0, np.inf, np.nan, -1.0, 5e-324, np.nextafter(1.0, 0)])])
+                        np.exp(rng.uniform(-745.0, 709.0, n)), nans,
+                        np.array([0.0, 1.0, np.inf, 5e-324, np.nextafter(1.0, 0)])])
     dev = eng.get_device(0)
-    for fn, name, xs in ((1, "log", x), (2, "log1p", np.concatenate([-x[:2 * n], x[2 * n:]]))):
+    for fn, name, xs in ((1, "log", x), (2, "log1p", np.concatenate([-x[:2 * n], x[2 * n:], [-1.0]]))):
         got = dev.libm(xs, fn)
         want = np.array([fns[name](float(v)) for v in xs])
-        same = (got.view(np.int64) == want.view(np.int64)) | (np.isnan(got) & np.isnan(want))
+        same = got.view(np.int64) == want.view(np.int64)  # NaNs too (an input NaN propagates)
         assert same.all(), (name, xs[~same][:5])
+    # negative arguments (never reached by the DP: p, 1 - p in [0, 1]) give a NaN of the
+    # hardware's own default encoding
+    assert np.isnan(dev.libm(np.array([-1.0, -2.5]), 1)).all()
 
 
 @pytest.mark.parametrize("seed", [30, 31])
@@ -566,3 +570,36 @@ def test_exact_logs_mode_same_scores(eng, seed, monkeypatch):
         ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 32)
         for f in range(nf):
             assert bits_equal(scores["1"][f * len(pens) + pi], ref["score"][:, f])
+
+
+def test_zero_pseudo_count_nan_bits_vs_oracle(eng):
+    """alpha = 0 with empty k-mers makes p = 0/0 (NaN) in some cells: every stored float32
+    equals the oracle's bit for bit, NaN encodings included (the C library's log lets an
+    input NaN through unchanged, and so must the GPU's restatement)."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    from oracle import oracle as O
+    rng = random.Random(77)
+    gp, ctx = _random_case(rng, 5)
+    for kmer in list(ctx)[::7]:
+        ctx[kmer] = (0, 0)
+    nf = 3
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(77), np.uint32)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr, utr = tot_m.sum() - tot_m, tot_u.sum() - tot_u
+    betas = (0.0 * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+    pens = [0.0, 4.0]
+    plan = eng.Plan(eng.get_device(0), gp, 0)
+    plan.set_counts(Mk, Uk)
+    plan.run([(f, 0.0, float(betas[f]), pens) for f in range(nf)])
+    nan_seen = False
+    for pi, c in enumerate(pens):
+        ref = O.cv_pass(gp, contexts, Mf, Uf, 0.0, betas, c, 32)
+        for f in range(nf):
+            score, _ = plan.dump_lane(f * len(pens) + pi)
+            assert np.array_equal(score.view(np.uint32), ref["score"][:, f].view(np.uint32)), (c, f)
+            nan_seen = nan_seen or bool(np.isnan(score).any())
+    plan.close()
+    assert nan_seen
