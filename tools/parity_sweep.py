@@ -2,7 +2,8 @@
 tests/test_gpu_parity.py's random cases).  Random IUPAC general patterns (k = 3..6, at
 most two N), random counts (zeros included), folds, pseudo counts, 1-8 penalties, block
 sizes and lanes per workgroup; every cell's float32 score and every root test value must
-equal the oracle's bit for bit.  usage: python tools/parity_sweep.py N_CASES SEED  (SWEEP_MAX_CELLS bounds the lattice)"""
+equal the oracle's bit for bit.  usage: python tools/parity_sweep.py N_CASES SEED  (SWEEP_MAX_CELLS bounds the lattice;
+SWEEP_U64=1 scales the counts past 2^32 so that every case takes the uint64 itype)"""
 import os
 import random
 import sys
@@ -19,6 +20,7 @@ from oracle import oracle as O  # noqa: E402
 
 
 MAX_CELLS = int(os.environ.get("SWEEP_MAX_CELLS", "300000"))
+U64 = os.environ.get("SWEEP_U64") == "1"
 
 
 def case(rng):
@@ -34,6 +36,9 @@ def case(rng):
         ctx[kmer] = (pos, bg - pos)
     if sum(v[0] for v in ctx.values()) == 0:
         ctx[next(iter(ctx))] = (5, 100)
+    if U64:  # totals past 2^32 - 1: the reference's uint64 itype (CV :94-97)
+        scale = (2 ** 33) // max(1, sum(m + u for m, u in ctx.values())) + 1
+        ctx = {k: (m * scale, u * scale) for k, (m, u) in ctx.items()}
     return gp, ctx
 
 
@@ -47,8 +52,9 @@ def main():
         gp, ctx = case(rng)
         nf = rng.choice([2, 3, 5])
         os.environ["KP_LANES_PER_WG"] = str(rng.choice([1, 2, 3, 4, 5, 5, 5, 6, 8]))
-        contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(i), np.uint32)
-        Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+        itype = np.uint64 if U64 else np.uint32
+        contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(i), itype)
+        Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), itype)
         alpha = rng.choice([0.0, 0.1, 1.0, 7.0])
         tot_m = Mf.sum(axis=0).astype(np.uint64)
         tot_u = Uf.sum(axis=0).astype(np.uint64)
@@ -61,7 +67,7 @@ def main():
         try:
             _, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
             for pi, c in enumerate(pens):
-                ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 32)
+                ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 64 if U64 else 32)
                 for f in range(nf):
                     lane = f * len(pens) + pi
                     score, _ = plan.dump_lane(lane)
