@@ -603,3 +603,32 @@ def test_zero_pseudo_count_nan_bits_vs_oracle(eng):
             nan_seen = nan_seen or bool(np.isnan(score).any())
     plan.close()
     assert nan_seen
+
+
+def test_negative_penalty_takes_exact_logs(eng):
+    """A group outside the fast path's premise (a negative penalty: the single term's parts
+    no longer all >= 0) takes the C library's logs for every cell: still the oracle's
+    scores bit for bit."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    from oracle import oracle as O
+    rng = random.Random(91)
+    gp, ctx = _random_case(rng, 5)
+    nf = 2
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(91), np.uint32)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    alpha = 0.5
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr, utr = tot_m.sum() - tot_m, tot_u.sum() - tot_u
+    betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+    pens = [-2.0, 3.0]
+    plan = eng.Plan(eng.get_device(0), gp, 0)
+    plan.set_counts(Mk, Uk)
+    plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
+    for pi, c in enumerate(pens):
+        ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 32)
+        for f in range(nf):
+            score, _ = plan.dump_lane(f * len(pens) + pi)
+            assert np.array_equal(score.view(np.uint32), ref["score"][:, f].view(np.uint32)), (c, f)
+    plan.close()
