@@ -60,3 +60,15 @@ def test_libm_log1p_restatement():
     got = _restated(x, 1)
     bad = ~_same(got, want)
     assert not bad.any(), (x[bad][:5], got[bad][:5], want[bad][:5])
+
+
+def test_scipy_xlogy_xlog1py_are_libm():
+    """The reference's k-mer terms call scipy.special.xlogy / xlog1py (CV module :15-20,
+    Fit :26-29); both are x times the C library's log / log1p (not scipy's own cephes
+    log1p, which differs in the last bit on ~7 % of inputs), so kp_libm.h restates them too."""
+    import scipy.special as sp
+    rng = np.random.RandomState(13)
+    p = rng.uniform(0.0, 1.0, 200_000)
+    u = rng.randint(1, 10**7, 200_000).astype(np.float64)
+    assert _same(sp.xlogy(u, p), u * _restated(p, 0)).all()
+    assert _same(sp.xlog1py(u, -p), u * _restated(-p, 1)).all()
