@@ -134,6 +134,11 @@ int kp_fit_leaves(kp_plan *plan, uint32_t lane, uint64_t *leaves, uint64_t cap, 
  * ([npat] each; either pointer may be NULL). */
 int kp_dump_lane(kp_plan *plan, uint32_t lane, float *score, uint8_t *code);
 
+/* Debug / parity: the train scores of the cells cells[0..n) (cell indices < npat) of lane
+ * `lane` of the last pass, into out[n] -- e.g. every cell of a sub-pattern embedded in a
+ * full-size lattice, whose values depend only on its own sub-lattice. */
+int kp_gather_cells(kp_plan *plan, uint32_t lane, const uint64_t *cells, uint64_t n, float *out);
+
 /* Parity check of the device's float64 log (the log of the single-pattern term, CV :61-62 /
  * Fit :56-57; ROCm's ocml): y[i] = log(x[i]) computed on the context's GPU. */
 int kp_math_log(kp_ctx *ctx, const double *x, double *y, uint64_t n);

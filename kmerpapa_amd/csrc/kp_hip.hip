@@ -334,6 +334,16 @@ __global__ void kp_libm_kernel(const double *__restrict__ x, double *__restrict_
         y[i] = fn == 1 ? kp_libm_log(x[i]) : fn == 2 ? kp_libm_log1p(x[i]) : log(x[i]);
 }
 
+// float32 scores of the given cells of one lane (parity checks of a full-size pass: the
+// cells of an embedded sub-lattice, against the oracle run on that sub-lattice alone)
+__global__ void kp_gather_cells_kernel(kp_geom g, const float *__restrict__ S, uint32_t lane,
+                                       const uint64_t *__restrict__ cells, uint64_t n, float *__restrict__ out) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t x = cells[i];
+        out[i] = S[kp_s_off(g, x / g.B, lane, (uint32_t)(x % g.B))];
+    }
+}
+
 // argmin code of every cell of one lane (parity dumps): the sequential decision of kp_core.h
 template <typename CT>
 __global__ void kp_codes_kernel(kp_geom g, kp_dev_tables T, const CT *K, const float *S, kp_group_dev G,
@@ -744,12 +754,13 @@ static int lanes_per_wg_default() {
 // (the driver wipes freed memory before handing it out again: ~4 s for 100-150 GB,
 // tools/alloc_probe.hip), so callers reserve the largest pass up front (kp_reserve_lanes).
 // ---- the score rows: the one very large allocation ----
-// A hipMalloc of HBM that was used before waits for the driver's wipe (~30 ms per GB).
-// The device's stream-ordered pool does not, but re-serving a freed pool block for a larger
-// request returned corrupt memory at >= 140 GB (tools/async_check.hip).  So: the FIRST score
-// buffer of a process on a device comes from the pool (nothing was ever freed there), is
-// written with a pattern and read back before use, and every later one (after a free, or
-// if the check fails) comes from hipMalloc.  KP_POOL_SCORES=0 disables the pool.
+// Plain hipMalloc.  A hipMalloc of HBM that was used before waits for the driver's wipe
+// (~30 ms per GB); the device's stream-ordered pool does not, but re-serving a freed pool
+// block for a larger request returned memory that does not hold what is written to it
+// (tools/async_check.hip), so the pool is NOT used by default.  Opt-in only
+// (KP_POOL_SCORES=1, for allocation-time experiments): then the FIRST score buffer of a
+// process on a device comes from the pool (nothing was ever freed there) and is written
+// with a pattern and read back before use; every later one comes from hipMalloc.
 static std::atomic<bool> g_pool_touched[64];
 
 __global__ void kp_fill_pattern(uint32_t *p, size_t n) {
@@ -780,7 +791,7 @@ static void free_scores(kp_plan *p) {
 static int alloc_scores(kp_plan *p, size_t bytes) {
     kp_ctx *c = p->ctx;
     const char *e = getenv("KP_POOL_SCORES");
-    const bool allow = !(e && atoi(e) == 0) && c->device >= 0 && c->device < 64;
+    const bool allow = e && atoi(e) == 1 && c->device >= 0 && c->device < 64;
     if (allow && !g_pool_touched[c->device].exchange(true)) {
         void *q = nullptr;
         if (hipMallocAsync(&q, bytes, c->stream) == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess) {
@@ -1145,6 +1156,38 @@ int kp_dump_lane(kp_plan *p, uint32_t lane, float *score, uint8_t *code) {
         }
     }
     if (code) return p->ct_bytes == 4 ? run_codes<uint32_t>(p, lane, code) : run_codes<uint64_t>(p, lane, code);
+    return KP_OK;
+}
+
+int kp_gather_cells(kp_plan *p, uint32_t lane, const uint64_t *cells, uint64_t n, float *out) {
+    if (!p || (n && (!cells || !out))) return fail(KP_E_ARG, "null argument");
+    if (lane >= p->last_ltot) return fail(KP_E_STATE, "lane not in last pass");
+    for (uint64_t i = 0; i < n; ++i)
+        if (cells[i] >= p->hp.npat) return fail(KP_E_ARG, "cell " + std::to_string(cells[i]) + " out of range");
+    if (!n) return KP_OK;
+    KP_HIP(hipSetDevice(p->ctx->device));
+    kp_ctx *c = p->ctx;
+    kp_geom g = p->hp.g;
+    g.Ltot = p->last_ltot;
+    const uint64_t chunk = std::min<uint64_t>(n, 1ull << 26);
+    uint64_t *d_cells = nullptr;
+    float *d_out = nullptr;
+    KP_HIP(dmalloc(&d_cells, chunk * sizeof(uint64_t)));
+    hipError_t e = dmalloc(&d_out, chunk * sizeof(float));
+    for (uint64_t i0 = 0; i0 < n && e == hipSuccess; i0 += chunk) {
+        const uint64_t m = std::min(chunk, n - i0);
+        e = hipMemcpyAsync(d_cells, cells + i0, m * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream);
+        if (e != hipSuccess) break;
+        const unsigned nb = (unsigned)std::min<uint64_t>((m + 255) / 256, 65536);
+        hipLaunchKernelGGL(kp_gather_cells_kernel, dim3(nb), dim3(256), 0, c->stream, g, p->d_S, lane, d_cells, m,
+                           d_out);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(out + i0, d_out, m * sizeof(float), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    dfree(d_cells);
+    dfree(d_out);
+    if (e != hipSuccess) return fail(KP_E_HIP, std::string("kp_gather_cells: ") + hipGetErrorString(e));
     return KP_OK;
 }
 

@@ -60,7 +60,7 @@ class KPPassStats(ctypes.Structure):
 
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
            "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
-           "kp_reserve_lanes", "kp_last_pass_stats", "kp_fit_leaves", "kp_dump_lane", "kp_fold_split",
+           "kp_reserve_lanes", "kp_last_pass_stats", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
            "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free"]
 
 
@@ -101,6 +101,7 @@ def load():
         L.kp_reserve_lanes.argtypes = [vp, ctypes.c_uint32]
         L.kp_fit_leaves.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u64p]
         L.kp_dump_lane.argtypes = [vp, ctypes.c_uint32, vp, vp]
+        L.kp_gather_cells.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, vp]
         L.kp_fold_split.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_int, vp]
         if hasattr(L, "kp_math_log"):  # (older builds loaded through KMERPAPA_LIB for A/B timing lack it)
             L.kp_math_log.argtypes = [vp, vp, vp, ctypes.c_uint64]
@@ -130,19 +131,45 @@ LAUNCH_KNOBS = ("KP_DP_THREADS", "KP_LANES_PER_WG", "KP_XCD_REMAP", "KP_LANE_SPL
                 "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER", "KP_EXACT_LOGS")
 
 
+_toolchain = None
+
+
+def toolchain_version():
+    """``hipcc --version`` text (the compiler that builds the library; part of kernel_tag)."""
+    global _toolchain
+    if _toolchain is None:
+        import subprocess
+        hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+        try:
+            _toolchain = subprocess.run([hipcc, "--version"], capture_output=True, text=True, timeout=60).stdout
+        except (OSError, subprocess.SubprocessError):
+            _toolchain = "hipcc: unavailable"
+    return _toolchain
+
+
 def kernel_tag():
-    """Short hash of everything that decides the sweep's launches: every source of the
-    library (csrc/*, the C-ABI header) and the launch knobs set in the environment.  Ties
-    PMC profiles (profiles/*/pmc_*.json) to the exact build and launch configuration."""
+    """Short hash of everything that decides the sweep's launches: the library's tracked
+    sources (csrc/kp_*.h, kp_*.hip, gen_logdata.py, Makefile, the C-ABI header), the log
+    constants generated into kp_logdata.h (without its comment lines, which name the host
+    libm's path), the compiler (``hipcc --version``) and the launch knobs set in the
+    environment.  Ties PMC profiles (profiles/*/pmc_*.json) to the exact build and launch
+    configuration."""
     import glob
     import hashlib
     h = hashlib.sha1()
-    files = sorted(glob.glob(os.path.join(_HERE, "csrc", "*")))
-    files.append(os.path.join(os.path.dirname(_HERE), "include", "kmerpapa_hip.h"))
+    csrc = os.path.join(_HERE, "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "kp_*.h")) + glob.glob(os.path.join(csrc, "kp_*.hip")))
+    files = [f for f in files if os.path.basename(f) != "kp_logdata.h"]
+    files += [os.path.join(csrc, "gen_logdata.py"), os.path.join(csrc, "Makefile"),
+              os.path.join(os.path.dirname(_HERE), "include", "kmerpapa_hip.h")]
     for fn in files:
-        if os.path.isfile(fn) and not fn.endswith((".s", ".o")):
-            with open(fn, "rb") as f:
-                h.update(os.path.basename(fn).encode() + b"\0" + f.read())
+        with open(fn, "rb") as f:
+            h.update(os.path.basename(fn).encode() + b"\0" + f.read())
+    gen = os.path.join(csrc, "kp_logdata.h")
+    if os.path.isfile(gen):
+        with open(gen, "rb") as f:
+            h.update(b"kp_logdata.h\0" + b"".join(x for x in f.readlines() if not x.lstrip().startswith(b"//")))
+    h.update(toolchain_version().encode())
     for k in LAUNCH_KNOBS:
         h.update(f"{k}={os.environ.get(k, '')}".encode())
     return h.hexdigest()[:12]
@@ -364,6 +391,14 @@ class Plan:
         code = np.zeros(self.info["npat"], np.uint8)
         _check(load().kp_dump_lane(self._h, int(lane), _ptr(score), _ptr(code)))
         return score, code
+
+    def gather_cells(self, lane, cells):
+        """Train scores (f32) of the cells ``cells`` (uint64 indices) of ``lane`` of the last
+        pass (kp_gather_cells)."""
+        cells = np.ascontiguousarray(cells, dtype=np.uint64).reshape(-1)
+        out = np.zeros(cells.size, np.float32)
+        _check(load().kp_gather_cells(self._h, int(lane), _ptr(cells), ctypes.c_uint64(cells.size), _ptr(out)))
+        return out
 
     def lanes_that_fit(self, reserve=2 << 30):
         fr, _ = self.device.mem()

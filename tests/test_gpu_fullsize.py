@@ -101,3 +101,226 @@ def test_9mer_full_cv_roots_monotone_in_penalty(counts):
     assert np.isfinite(rt).all() and (np.diff(rt) >= -1e-6 * np.abs(rt[1:])).all()
     assert (np.diff(np.asarray(nl, np.int64)) <= 0).all()  # fewer (or equal) patterns as c grows
     assert np.isfinite(np.asarray(re)).all()
+
+
+# ---------------------------------------------------------------------------------------
+# Full-size CV lanes pinned cell by cell: a cell's DP value depends only on its own
+# sub-lattice (the k-mers it matches, their fold counts, alpha, beta_f and c: CV :26-78),
+# so every cell of a sub-pattern S embedded in NNNNMNNNN must equal the oracle's value of
+# the same pattern in a run on the lattice of S alone, given the FULL run's fold counts
+# and betas.  The oracle runs one fold as a 2-column table [fold f, all other folds]:
+# train = sum of columns - column 0 = all data - fold f (CV :22-24, :56-59), exactly the
+# full run's train counts of fold f, at a fifth of the work of all five folds.
+# ---------------------------------------------------------------------------------------
+
+@pytest.fixture(scope="module")
+def cv_split(counts):
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    kmers, M, U = counts
+    ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
+    contexts, Mf, Uf = fold_tables(ctx, 5, np.random.RandomState(1), np.uint32)
+    Mk, Uk = engine.counts_in_kmer_order(GEN_PAT, contexts, Mf, Uf, generality(GEN_PAT), np.uint32)
+    msum, usum = Mk.sum(axis=0, dtype=np.uint64), Uk.sum(axis=0, dtype=np.uint64)
+    return {"contexts": contexts, "Mf": Mf, "Uf": Uf, "Mk": Mk, "Uk": Uk,
+            "mtr": msum.sum() - msum, "utr": usum.sum() - usum}
+
+
+def _embedded_cells(full, sub):
+    """Full-lattice index of every cell of the sub-lattice ``sub`` (in the sub-lattice's own
+    index order), from the oracle's IUPAC tables (mixed radix, position 0 fastest)."""
+    from oracle.oracle import _PERM
+    n = 1
+    for g in sub:
+        n *= len(_PERM[g])
+    x = np.arange(n, dtype=np.int64)
+    out = np.zeros(n, np.uint64)
+    w = 1
+    for g, s in zip(full, sub):
+        r = len(_PERM[s])
+        lut = np.array([_PERM[g].index(ch) for ch in _PERM[s]], np.uint64)
+        out += lut[x % r] * np.uint64(w)
+        x //= r
+        w *= len(_PERM[g])
+    return out
+
+
+IUPAC = {"A": "A", "C": "C", "G": "G", "T": "T", "R": "AG", "Y": "CT", "S": "CG", "W": "AT", "K": "GT",
+         "M": "AC", "B": "CGT", "D": "AGT", "H": "ACT", "V": "ACG", "N": "ACGT"}
+
+SUBS = ["ANNNMNNNA",   # low in the index space
+        "AANNMNNNV"]   # last position V: cells at index >= 13/15 * npat > 2^32
+
+
+@pytest.mark.timeout(1200)
+def test_9mer_full_cv_lane_embedded_sublattices_vs_oracle(cv_split):
+    """One 5-lane (alpha, fold) group of the headline CV pass over the whole 9-mer lattice
+    (7.69e9 cells, default block: 6 high positions, 17 launches): every cell of two
+    embedded sub-lattices (ANNNMNNNA: 3.4e7 cells; AANNMNNNV: 1.6e7 cells at cell indices
+    and score-buffer offsets past 2^32) equals the oracle bit for bit in all 5 lanes."""
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.score_utils import get_betas
+    from oracle import oracle as O
+    from tests.fixtures import bits_equal
+    sp = cv_split
+    alpha, fold, pens = 2.0, 3, [3.0, 4.0, 5.0, 6.0, 7.0]
+    betas = get_betas(alpha, sp["mtr"], sp["utr"])
+    plan = engine.get_plan(engine.visible_devices()[0], GEN_PAT, 0)
+    assert plan.info["npat"] == 7688671875 and plan.info["high_levels"] > 1
+    plan.set_counts(sp["Mk"], sp["Uk"])
+    plan.run([(fold, alpha, float(betas[fold]), pens)])
+    assert plan.stats()["dp_launches"] == 17
+    bf = float(betas[fold])
+    for sub in SUBS:
+        keep = [i for i, c in enumerate(sp["contexts"]) if all(c[j] in IUPAC[ch] for j, ch in enumerate(sub))]
+        ctxs = [sp["contexts"][i] for i in keep]
+        mf, uf = sp["Mf"][keep], sp["Uf"][keep]
+        m2 = np.stack([mf[:, fold], mf.sum(axis=1) - mf[:, fold]], axis=1)
+        u2 = np.stack([uf[:, fold], uf.sum(axis=1) - uf[:, fold]], axis=1)
+        cells = _embedded_cells(GEN_PAT, sub)
+        assert cells.size == O.npat(sub)
+        if sub == "AANNMNNNV":
+            assert (cells > 2 ** 32).sum() > cells.size // 4  # last digit M or V: index > 2^32
+        for j, c in enumerate(pens):
+            ref = O.cv_pass(sub, ctxs, m2, u2, alpha, [bf, bf], c, 32, threads=_threads())
+            got = plan.gather_cells(j, cells)
+            assert bits_equal(got, ref["score"][:, 0]), (sub, c, int(np.sum(got.view(np.uint32) !=
+                                                                             ref["score"][:, 0].view(np.uint32))))
+            del ref
+
+
+def _threads():
+    import os
+    n = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    return max(1, min(n, 16))
+
+
+def _leaf_kmers(gen_pat, leaves):
+    """(leaf number, k-mer index) of every k-mer every leaf cell matches, vectorised: the
+    leaf cells are decoded to IUPAC letters (oracle tables) and expanded position by
+    position; k-mer index = KmerEnumeration order (position 0 fastest, digit = rank of the
+    nucleotide among the general code's nucleotides, alphabetical)."""
+    from oracle.oracle import _PERM
+    x = np.asarray(leaves, np.int64).copy()
+    codes = []
+    for g in gen_pat:
+        r = len(_PERM[g])
+        codes.append(x % r)
+        x //= r
+    leaf = np.arange(len(leaves), dtype=np.int64)
+    kidx = np.zeros(len(leaves), np.int64)
+    w = 1
+    for i, g in enumerate(gen_pat):
+        nucs = IUPAC[g]
+        # per sub-code of g: its nucleotides' digits (padded with -1)
+        tab = np.full((len(_PERM[g]), 4), -1, np.int64)
+        size = np.zeros(len(_PERM[g]), np.int64)
+        for d, ch in enumerate(_PERM[g]):
+            ds = [nucs.index(n) for n in IUPAC[ch]]
+            tab[d, :len(ds)] = ds
+            size[d] = len(ds)
+        code_i = codes[i][leaf]
+        rep = size[code_i]
+        start = np.cumsum(rep) - rep
+        leaf = np.repeat(leaf, rep)
+        kidx = np.repeat(kidx, rep)
+        j = np.arange(leaf.size) - np.repeat(start, rep)
+        kidx = kidx + tab[codes[i][leaf], j] * w
+        w *= len(nucs)
+    return leaf, kidx
+
+
+@pytest.mark.timeout(1200)
+def test_9mer_full_cv_all_125_lanes_leaf_sums(cv_split):
+    """The whole 5x5x5 headline grid (25 passes of 5 lanes over 7.69e9 cells): for every
+    lane, the optimal partition (kp_fit_leaves) covers each k-mer exactly once, the root
+    train value equals the float64 sum of the leaves' single-pattern train terms and the
+    root test value the float64 sum of their test terms (CV :60-78, :158-163), both within
+    the float32 summation error of a tree of at most max_level + 1 levels."""
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.score_utils import get_betas
+    sp = cv_split
+    alphas, pens, nf = [0.5, 1.0, 2.0, 5.0, 10.0], [3.0, 4.0, 5.0, 6.0, 7.0], 5
+    plan = engine.get_plan(engine.visible_devices()[0], GEN_PAT, 0)
+    plan.set_counts(sp["Mk"], sp["Uk"])
+    nk = plan.info["n_kmers"]
+    Mk = sp["Mk"].astype(np.int64)
+    Uk = sp["Uk"].astype(np.int64)
+    Mall, Uall = Mk.sum(axis=1), Uk.sum(axis=1)
+    tol = (plan.info["max_level"] + 2) * 2.0 ** -24
+    checked = 0
+    for a in alphas:
+        betas = get_betas(a, sp["mtr"], sp["utr"])
+        for f in range(nf):
+            beta = float(betas[f])
+            rt, re, nl = plan.run([(f, a, beta, pens)])
+            mte_k, ute_k = Mk[:, f], Uk[:, f]
+            mtr_k, utr_k = Mall - mte_k, Uall - ute_k
+            for j, c in enumerate(pens):
+                leaves = plan.leaves(j)
+                assert leaves.size == int(nl[j])
+                leaf, kidx = _leaf_kmers(GEN_PAT, leaves)
+                assert kidx.size == nk and (np.bincount(kidx, minlength=nk) == 1).all(), (a, f, c)
+                n = leaves.size
+                sums = [np.bincount(leaf, weights=v[kidx].astype(np.float64), minlength=n)
+                        for v in (mtr_k, utr_k, mte_k, ute_k)]
+                mtr, utr, mte, ute = sums
+                single = np.bincount(leaf, minlength=n) == 1
+                p = (mtr + a) / (((mtr + utr) + a) + beta)
+                lp, l1p = np.log(p), np.log(1.0 - p)
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    tr_wide = c + np.where(mtr > 0, (-2.0 * mtr) * lp, 0.0) + np.where(utr > 0, (-2.0 * utr) * l1p, 0.0)
+                    te_wide = np.where(mte > 0, (-2.0 * mte) * lp, 0.0) + np.where(ute > 0, (-2.0 * ute) * l1p, 0.0)
+                    l1p_k = np.log1p(-p)
+                    tr_k = -2.0 * (np.where(mtr > 0, mtr * lp, 0.0) + np.where(utr > 0, utr * l1p_k, 0.0)) + c
+                    te_k = -2.0 * (np.where(mte > 0, mte * lp, 0.0) + np.where(ute > 0, ute * l1p_k, 0.0))
+                train = float(np.where(single, tr_k, tr_wide).sum())
+                test = float(np.where(single, te_k, te_wide).sum())
+                assert abs(float(rt[j]) - train) <= tol * abs(train), (a, f, c, float(rt[j]), train)
+                assert abs(float(re[j]) - test) <= tol * abs(test), (a, f, c, float(re[j]), test)
+                checked += 1
+    assert checked == 125
+
+
+@pytest.mark.timeout(900)
+def test_9mer_full_lane_buffer_grow_sequence(cv_split):
+    """The product's allocation sequence at full size: a fresh plan reserves 2 lanes
+    (61 GB of score rows), runs a 2-lane pass, grows to 5 lanes (154 GB: the 2-lane buffer
+    is freed and a larger one allocated -- the sequence that made the stream-ordered pool
+    return memory not holding what was written), runs a 5-lane pass; after
+    each pass every cell of the embedded sub-lattice AANNMNNNV (offsets past 2^32) equals
+    the oracle in the first and last lane."""
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.score_utils import get_betas
+    from oracle import oracle as O
+    from tests.fixtures import bits_equal
+    sp = cv_split
+    engine.release_all()
+    alpha, fold = 5.0, 1
+    bf = float(get_betas(alpha, sp["mtr"], sp["utr"])[fold])
+    sub = "AANNMNNNV"
+    keep = [i for i, c in enumerate(sp["contexts"]) if all(c[j] in IUPAC[ch] for j, ch in enumerate(sub))]
+    ctxs = [sp["contexts"][i] for i in keep]
+    mf, uf = sp["Mf"][keep], sp["Uf"][keep]
+    m2 = np.stack([mf[:, fold], mf.sum(axis=1) - mf[:, fold]], axis=1)
+    u2 = np.stack([uf[:, fold], uf.sum(axis=1) - uf[:, fold]], axis=1)
+    cells = _embedded_cells(GEN_PAT, sub)
+    ref = {}
+    plan = engine.Plan(engine.get_device(engine.visible_devices()[0]), GEN_PAT, 0)
+    try:
+        plan.set_counts(sp["Mk"], sp["Uk"])
+        for pens in ([3.5, 6.5], [3.0, 4.0, 5.0, 6.0, 7.0]):
+            plan.reserve(len(pens))
+            plan.run([(fold, alpha, bf, pens)])
+            for j in (0, len(pens) - 1):
+                c = pens[j]
+                if c not in ref:
+                    ref[c] = O.cv_pass(sub, ctxs, m2, u2, alpha, [bf, bf], c, 32, threads=_threads())["score"][:, 0]
+                assert bits_equal(plan.gather_cells(j, cells), ref[c]), (len(pens), c)
+    finally:
+        plan.close()
