@@ -294,27 +294,69 @@ def cv_run(plan, prep, gen_pat, groups):
             "fold_split_s": box["t_fold"][-1], "passes_start_s": t_start, "lanes": sum(len(g[3]) for g in groups)}
 
 
-def full_cv(plan, prep, gen_pat, rank, world, cap, model_world=8):
+def shadow_host_side(prep, gen_pat, device):
+    """The host work every rank of a multi-GPU job does before and beside its passes (cv_run
+    without the passes): the plan's table build and upload, the all-data counts in k-mer
+    order and the whole fold split drawn fold by fold.  Run by the N - 1 other "ranks" of a
+    modelled world while one rank's share runs for real, so that share sees the host
+    contention of N concurrent ranks (threads of one process: they also share one GIL,
+    which makes the model pessimistic against N separate processes)."""
+    from kmerpapa_amd.CV_tools import all_counts, fold_stream
+    nf, itype = prep["nfolds"], prep["itype"]
+    p = engine.Plan(device, gen_pat, 0)
+    nk = p.info["n_kmers"]
+    contexts, Ma, Ua = all_counts(prep["ctx"], itype)
+    idx = engine.kmer_order(gen_pat, contexts)
+    M_all = np.zeros(nk, itype)
+    M_all[idx] = Ma
+    for f, Mf, Uf in fold_stream(prep["ctx"], nf, np.random.RandomState(1), itype):
+        mk = np.zeros(nk, itype)
+        mk[idx] = Mf
+    p.close()
+
+
+def model_world(plan, prep, gen_pat, world):
+    """Modelled wall-clock of the full CV on ``world`` GPUs: every rank's lane-granular share
+    (shard.rank_groups) is run as that rank runs it (cv_run: its own pipelined fold split,
+    table build and passes), one share after the other on this GPU, each while world - 1
+    shadow threads do the other ranks' host side at the same time (shadow_host_side).  Only
+    the GPU part is serialised; there is no data-path collective, so the
+    job's wall-clock is the slowest share."""
+    import threading
+    from kmerpapa_amd.shard import rank_groups
+    shares = []
+    for r in range(world):
+        shadows = [threading.Thread(target=shadow_host_side, args=(prep, gen_pat, plan.device))
+                   for _ in range(world - 1)]
+        for th in shadows:
+            th.start()
+        shares.append(cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], r, world)))
+        for th in shadows:
+            th.join()
+    return {"world": world, "share_s": [round(x["wall_s"], 4) for x in shares],
+            "share_lanes": [x["lanes"] for x in shares],
+            "share_passes_start_s": [round(x["passes_start_s"], 4) for x in shares],
+            "share_fold_split_s": [round(x["fold_split_s"], 4) for x in shares],
+            "wall_s": max(x["wall_s"] for x in shares)}
+
+
+def full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds=(2, 4, 8)):
     """The whole grid x folds as the CV driver runs it (cv_run: pipelined fold split,
     this rank's lane-granular share of the passes in fold order, root read-out) on the plan
     the timed steps used.  The one-time HBM allocation is not in the wall-clock
     (``prep["t_alloc"]``, reported beside it: on this platform it is dominated by the
     driver wiping HBM that earlier processes freed, 0.05-6 s for 150 GB).  At world 1 it
-    also runs, one after the other on the same GPU, the shares the ``model_world`` ranks
-    of an 8-GPU job would get -- each with its own pipelined fold split, as every rank
-    draws it -- and models that job's wall-clock as the slowest share (there is no
-    data-path collective)."""
+    also models the wall-clock of a job on 2, 4 and 8 GPUs (model_world)."""
     from kmerpapa_amd.shard import rank_groups
     out = cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], rank, world))
     out["hbm_alloc_s"] = prep["t_alloc"]
     out["wall_s_incl_alloc"] = out["wall_s"] + prep["t_alloc"]
-    if world == 1 and model_world > 1:
-        shares = [cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], r, model_world))
-                  for r in range(model_world)]
-        out["model"] = {"world": model_world, "share_s": [round(x["wall_s"], 4) for x in shares],
-                        "share_lanes": [x["lanes"] for x in shares],
-                        "share_passes_start_s": [round(x["passes_start_s"], 4) for x in shares],
-                        "wall_s": max(x["wall_s"] for x in shares)}
+    if world == 1:
+        out["models"] = {}
+        for w in model_worlds:
+            m = model_world(plan, prep, gen_pat, w)
+            m["speedup"] = out["wall_s"] / m["wall_s"]
+            out["models"][str(w)] = m
     return out
 
 
@@ -364,7 +406,7 @@ def main():
     plan = engine.get_plan(prep["device"], gen_pat, a.max_block)
     prep["t_plan"] = time.perf_counter() - t0
     cap = engine.pass_cap(groups, plan.lanes_that_fit())
-    worlds = () if a.no_full_cv else ((world, 8) if world == 1 else (world,))
+    worlds = () if a.no_full_cv else ((world, 2, 4, 8) if world == 1 else (world,))
     most = max([len(groups[0][3])] + [sum(len(g[3]) for g in p) for w in worlds
                                       for passes in cv_shares(prep, w, cap) for p in passes])
     t0 = time.perf_counter()
@@ -462,9 +504,12 @@ def main():
 
             "kernel_tag": tag,
         }
-        if cv and "model" in cv:
-            line["cv_full_grid_wall_s_model_8gpu"] = cv["model"]["wall_s"]
-            line["cv_full_grid_speedup_model_8gpu"] = cv["wall_s"] / cv["model"]["wall_s"]
+        if cv and "models" in cv:
+            line["cv_full_grid_wall_s_model"] = {w: m["wall_s"] for w, m in cv["models"].items()}
+            line["cv_full_grid_speedup_model"] = {w: m["speedup"] for w, m in cv["models"].items()}
+            if "8" in cv["models"]:
+                line["cv_full_grid_wall_s_model_8gpu"] = cv["models"]["8"]["wall_s"]
+                line["cv_full_grid_speedup_model_8gpu"] = cv["models"]["8"]["speedup"]
         if not a.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(prep)
         else:

@@ -27,6 +27,7 @@
  *                    kp_fold_sample: one fold of it (sample :5-27)
  *   kp_kmer_parse    io_utils.py read_dict :82-136 (with downsize_contextD's centring,
  *                    :50-79) and read_joint_kmer_counts :3-46 (host code)
+ *   kp_format_long_rows  the -l rows of cli.py:301-316 (host code)
  */
 #ifndef KMERPAPA_HIP_H
 #define KMERPAPA_HIP_H
@@ -180,6 +181,19 @@ int kp_kmer_table_info(const kp_kmer_table *t, uint64_t *n, int32_t *k, int64_t 
 /* codes[n], c0[n], c1[n]: caller-allocated (n from kp_kmer_table_info) */
 int kp_kmer_table_copy(const kp_kmer_table *t, uint64_t *codes, int64_t *c0, int64_t *c1);
 void kp_kmer_table_free(kp_kmer_table *t);
+
+/* The long output table (host code, no GPU): cli.py:301-316 with -l prints, for every k-mer
+ * of every pattern, f"{context} {c_neg} {c_pos} {c_rate}" + the pattern's tail
+ * " {pattern} {p_neg} {p_pos} {p_rate}\n", c_rate = c_pos / (c_pos + c_neg) as Python's
+ * repr() writes a float.  kmers: n * k letters; pid[i] = row i's tail; tail t is
+ * tails[tail_off[t] .. tail_off[t + 1]).  Writes at most cap bytes to out, *out_len = bytes
+ * written.  KP_E_ARG if cap is too small or a row has c_pos + c_neg == 0 (where Python
+ * raises ZeroDivisionError). */
+int kp_format_long_rows(const char *kmers, int k, const int64_t *c_neg, const int64_t *c_pos, const uint32_t *pid,
+                        uint64_t n, const char *tails, const uint64_t *tail_off, uint64_t n_tails, char *out,
+                        uint64_t cap, uint64_t *out_len);
+/* Python repr() of x[0..n), one per line (the float format of kp_format_long_rows). */
+int kp_py_repr(const double *x, uint64_t n, char *out, uint64_t cap, uint64_t *out_len);
 
 #ifdef __cplusplus
 }

@@ -14,6 +14,8 @@ import sys
 import time
 from math import log
 
+import numpy as np
+
 from . import __version__
 from .algorithms import all_kmers_CV, bottum_up_array_penalty_plus_pseudo_CV, bottum_up_array_w_numba
 from .io_utils import read_input_table
@@ -104,6 +106,34 @@ class _Phases:
                    total_s=round(time.perf_counter() - self.t0, 4))
         with open(path, "a") as fh:
             fh.write(json.dumps(rec) + "\n")
+
+
+def write_partition(out, names, counts, contextD, alpha, beta, long_output):
+    """The output table (cli.py:301-316): one row per pattern ``pattern p_neg p_pos p_rate``,
+    or with ``-l`` one row per k-mer of each pattern (``matches`` order) ``context c_neg c_pos
+    c_rate pattern p_neg p_pos p_rate``; rates are Python float reprs.  The -l rows are built
+    from the table's arrays for all patterns at once (KmerCounts.partition_rows) and
+    formatted natively (engine.format_long_rows, the same text as the reference's f-string)."""
+    if long_output:
+        print("context", "c_neg", "c_pos", "c_rate", "pattern", "p_neg", "p_pos", "p_rate", file=out)
+        tails = [f" {pat} {Up} {Mp} {(Mp + alpha) / (Mp + Up + alpha + beta)}\n" for pat, (Mp, Up) in zip(names, counts)]
+        codes, pid = contextD.partition_rows(names)
+        idx = np.searchsorted(contextD.codes, codes)
+        from .engine import format_long_rows
+        from .io_utils import KmerCounts
+        rows = KmerCounts(contextD.k, codes, contextD.M[idx], contextD.U[idx])
+        text = format_long_rows(rows.letters(), rows.U, rows.M, pid, tails)
+        out.flush()
+        if hasattr(out, "buffer"):
+            out.buffer.write(text)
+            out.buffer.flush()
+        else:
+            out.write(text.decode("ascii"))
+    else:
+        print("pattern", "p_neg", "p_pos", "p_rate", file=out)
+        for pat, (Mp, Up) in zip(names, counts):
+            p = (Mp + alpha) / (Mp + Up + alpha + beta)
+            print(pat, Up, Mp, p, file=out)
 
 
 def main(args=None):
@@ -228,19 +258,7 @@ def main(args=None):
         print(f"loss={best_score}", file=sys.stderr)
         print(f"LL={get_loss(counts, best_alpha, best_beta)}", file=sys.stderr)
 
-    out = args.output
-    if args.long_output:
-        print("context", "c_neg", "c_pos", "c_rate", "pattern", "p_neg", "p_pos", "p_rate", file=out)
-    else:
-        print("pattern", "p_neg", "p_pos", "p_rate", file=out)
-    for pat, (Mp, Up) in zip(names, counts):
-        p = (Mp + best_alpha) / (Mp + Up + best_alpha + best_beta)
-        if args.long_output:  # one row per k-mer of the pattern, matches() order (cli.py:305-311)
-            tail = f" {pat} {Up} {Mp} {p}\n"
-            rows = ([pat], [Mp], [Up]) if len(names) == len(contextD) else contextD.match_rows(pat)
-            out.write("".join(f"{context} {ns} {nm} {float(nm) / (nm + ns)}{tail}" for context, nm, ns in zip(*rows)))
-        else:
-            print(pat, Up, Mp, p, file=out)
+    write_partition(args.output, names, counts, contextD, best_alpha, best_beta, args.long_output)
     clock.mark("output")
     clock.write(gen_pat=gen_pat, patterns=len(names), best_alpha=best_alpha, best_penalty=best_penalty)
     return 0

@@ -40,6 +40,7 @@
 #include "kp_dp_kernel.h"
 #include "kp_folds.h"
 #include "kp_io.h"
+#include "kp_out.h"
 #include "kp_plan.h"
 
 
@@ -377,10 +378,17 @@ static int fail(int code, const std::string &msg) {
             return fail(KP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));                 \
     } while (0)
 
+#define KP_SIDE_STREAMS 3
+
 struct kp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // side streams: the lane classes of one pass (device groups of different widths, e.g. a
+    // 5-lane and a 1-lane group, or the 4 + 3 split of a 7-penalty group) are independent,
+    // so each class runs its launch sequence on a stream of its own and the classes overlap
+    hipStream_t side[KP_SIDE_STREAMS] = {nullptr, nullptr, nullptr};
+    hipEvent_t side_ev[KP_SIDE_STREAMS] = {nullptr, nullptr, nullptr};
     size_t lds_max = 65536;
 };
 
@@ -490,6 +498,10 @@ int kp_create(int device, kp_ctx **out) {
     c->device = device;
     KP_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (auto &e : c->ev) KP_HIP(hipEventCreate(&e));
+    for (int i = 0; i < KP_SIDE_STREAMS; ++i) {
+        KP_HIP(hipStreamCreateWithFlags(&c->side[i], hipStreamNonBlocking));
+        KP_HIP(hipEventCreateWithFlags(&c->side_ev[i], hipEventDisableTiming));
+    }
     int lds = 0;
     if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds > 0)
         c->lds_max = (size_t)lds;
@@ -512,6 +524,10 @@ void kp_destroy(kp_ctx *c) {
     (void)hipSetDevice(c->device);
     for (auto e : c->ev)
         if (e) (void)hipEventDestroy(e);
+    for (int i = 0; i < KP_SIDE_STREAMS; ++i) {
+        if (c->side_ev[i]) (void)hipEventDestroy(c->side_ev[i]);
+        if (c->side[i]) (void)hipStreamDestroy(c->side[i]);
+    }
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -702,11 +718,11 @@ static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
 }
 
 template <typename CT, int NL, bool HZ>
-static int launch_dp_hz(kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
+static int launch_dp_hz(hipStream_t st, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
     if (lds > 65536)
         KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_kernel<CT, NL, HZ>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((kp_dp_kernel<CT, NL, HZ>), dim3(nb, ngroups), dim3(threads), lds, c->stream, P);
+    hipLaunchKernelGGL((kp_dp_kernel<CT, NL, HZ>), dim3(nb, ngroups), dim3(threads), lds, st, P);
     KP_HIP(hipGetLastError());
     return KP_OK;
 }
@@ -715,13 +731,13 @@ static int launch_dp_hz(kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned 
 // k-mer code (fewer spills: 1-lane pass 149 -> 144 ms); wider groups keep one kernel for
 // every level (the split build measured slower there: 5 lanes 395 -> 402 ms)
 template <typename CT, int NL>
-static int launch_dp(kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
-    return (P.H == 0 || NL > 3) ? launch_dp_hz<CT, NL, true>(c, P, nb, ngroups, threads, lds)
-                                : launch_dp_hz<CT, NL, false>(c, P, nb, ngroups, threads, lds);
+static int launch_dp(hipStream_t st, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
+    return (P.H == 0 || NL > 3) ? launch_dp_hz<CT, NL, true>(st, P, nb, ngroups, threads, lds)
+                                : launch_dp_hz<CT, NL, false>(st, P, nb, ngroups, threads, lds);
 }
 
 template <typename CT>
-static int launch_dp_nl(int nl, kp_ctx *c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads,
+static int launch_dp_nl(int nl, hipStream_t c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads,
                         size_t lds) {
     switch (nl) {
         case 1: return launch_dp<CT, 1>(c, P, nb, ngroups, threads, lds);
@@ -959,28 +975,48 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.stamps = d_stamps;
 #endif
     KP_HIP(hipEventRecord(c->ev[0], c->stream));
+    // lane classes: runs of device groups with equal lane counts (dg is sorted by width);
+    // one launch per (class, high level).  With several classes, class q > 0 runs its whole
+    // launch sequence on side stream q - 1 (KP_CLASS_STREAMS=0: everything on one stream)
+    std::vector<std::pair<size_t, size_t>> classes;
+    for (size_t i = 0; i < dg.size();) {
+        size_t j = i;
+        while (j < dg.size() && dg[j].nl == dg[i].nl) ++j;
+        classes.emplace_back(i, j);
+        i = j;
+    }
+    const bool multi = classes.size() > 1 && !(getenv("KP_CLASS_STREAMS") && atoi(getenv("KP_CLASS_STREAMS")) == 0);
+    if (multi) {
+        KP_HIP(hipEventRecord(c->ev[3], c->stream));
+        for (size_t q = 1; q < classes.size() && q <= KP_SIDE_STREAMS; ++q)
+            KP_HIP(hipStreamWaitEvent(c->side[q - 1], c->ev[3], 0));
+    }
     uint64_t launches = 0;
-    for (int H = 0; H <= hp.hmax; ++H) {
-        uint64_t nb = hp.hoff[H + 1] - hp.hoff[H];
-        if (!nb) continue;
-        P.hbase = hp.hoff[H];
-        P.H = H;
-        for (size_t i = 0; i < dg.size();) {
-            size_t j = i;
-            while (j < dg.size() && dg[j].nl == dg[i].nl) ++j;
+    for (size_t q = 0; q < classes.size(); ++q) {
+        const hipStream_t st = (multi && q > 0) ? c->side[(q - 1) % KP_SIDE_STREAMS] : c->stream;
+        const size_t i = classes[q].first, j = classes[q].second;
+        for (int H = 0; H <= hp.hmax; ++H) {
+            uint64_t nb = hp.hoff[H + 1] - hp.hoff[H];
+            if (!nb) continue;
             kp_dp_params Q = P;
+            Q.hbase = hp.hoff[H];
+            Q.H = H;
             Q.groups = p->d_groups + i;
             size_t lds = dp_lds_bytes(hp, dg[i].nl, sizeof(CT));
 #ifdef KP_ABLATION
             // ablation build only: extra LDS per workgroup to force lower occupancy
             if (getenv("KP_LDS_PAD")) lds += (size_t)atol(getenv("KP_LDS_PAD"));
 #endif
-            int rc = launch_dp_nl<CT>(dg[i].nl, c, Q, (unsigned)nb, (unsigned)(j - i), threads, lds);
+            int rc = launch_dp_nl<CT>(dg[i].nl, st, Q, (unsigned)nb, (unsigned)(j - i), threads, lds);
             if (rc) return rc;
             ++launches;
-            i = j;
         }
     }
+    if (multi)
+        for (size_t q = 1; q < classes.size() && q <= KP_SIDE_STREAMS; ++q) {
+            KP_HIP(hipEventRecord(c->side_ev[q - 1], c->side[q - 1]));
+            KP_HIP(hipStreamWaitEvent(c->stream, c->side_ev[q - 1], 0));
+        }
     KP_HIP(hipEventRecord(c->ev[1], c->stream));
     // breadth-first backtrack of every lane: depth d holds cells of level <= maxlev - d
     kp_bt_params B;
@@ -1307,5 +1343,31 @@ int kp_kmer_table_copy(const kp_kmer_table *t, uint64_t *codes, int64_t *c0, int
 }
 
 void kp_kmer_table_free(kp_kmer_table *t) { delete t; }
+
+// ---- the long output table (host code) ----
+int kp_format_long_rows(const char *kmers, int k, const int64_t *c_neg, const int64_t *c_pos, const uint32_t *pid,
+                        uint64_t n, const char *tails, const uint64_t *tail_off, uint64_t n_tails, char *out,
+                        uint64_t cap, uint64_t *out_len) {
+    if (!out_len || k < 1 || (n && (!kmers || !c_neg || !c_pos || !pid || !tails || !tail_off || !out)))
+        return fail(KP_E_ARG, "bad arguments");
+    const int64_t w = kpout::long_rows(kmers, k, c_neg, c_pos, pid, n, tails, tail_off, n_tails, out, cap);
+    if (w == -1) return fail(KP_E_ARG, "output buffer too small");
+    if (w == -2) return fail(KP_E_ARG, "division by zero: a k-mer with no counts in the long output");
+    if (w == -3) return fail(KP_E_ARG, "pattern index out of range");
+    *out_len = (uint64_t)w;
+    return KP_OK;
+}
+
+int kp_py_repr(const double *x, uint64_t n, char *out, uint64_t cap, uint64_t *out_len) {
+    if (!out_len || (n && (!x || !out))) return fail(KP_E_ARG, "bad arguments");
+    uint64_t w = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (w + 40 > cap) return fail(KP_E_ARG, "output buffer too small");
+        w += (uint64_t)kpout::py_repr(x[i], out + w);
+        out[w++] = '\n';
+    }
+    *out_len = w;
+    return KP_OK;
+}
 
 }  // extern "C"

@@ -61,7 +61,8 @@ class KPPassStats(ctypes.Structure):
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
            "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
            "kp_reserve_lanes", "kp_last_pass_stats", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
-           "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free"]
+           "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free",
+           "kp_format_long_rows", "kp_py_repr"]
 
 
 def load():
@@ -107,6 +108,9 @@ def load():
             L.kp_math_log.argtypes = [vp, vp, vp, ctypes.c_uint64]
         if hasattr(L, "kp_math_libm"):
             L.kp_math_libm.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int]
+        L.kp_format_long_rows.argtypes = [vp, ctypes.c_int, vp, vp, vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp,
+                                          ctypes.c_uint64, u64p]
+        L.kp_py_repr.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint64, u64p]
         L.kp_fold_sample.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_uint64, vp]
         for name in EXPORTS:
             if not hasattr(L, name):
@@ -128,7 +132,8 @@ def _ptr(a):
 
 # launch knobs read by kp_hip.hip (every setting gives the same scores; they change timing)
 LAUNCH_KNOBS = ("KP_DP_THREADS", "KP_LANES_PER_WG", "KP_XCD_REMAP", "KP_LANE_SPLIT", "KP_NT_STORE", "KP_NT_SLOW",
-                "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER", "KP_EXACT_LOGS")
+                "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER", "KP_EXACT_LOGS",
+               "KP_CLASS_STREAMS")
 
 
 _toolchain = None
@@ -236,6 +241,46 @@ def parse_kmer_counts(text, columns, super_pattern=None, length=0):
     finally:
         L.kp_kmer_table_free(t)
     return k.value, codes, c0, c1, t0.value, t1.value
+
+
+def py_repr(x):
+    """Python repr() of every float64 in ``x`` by the native formatter (kp_py_repr); a list
+    of str.  Host code, no GPU (a check of kp_format_long_rows' float format)."""
+    x = np.ascontiguousarray(x, dtype=np.float64).reshape(-1)
+    cap = 40 * x.size + 1
+    buf = ctypes.create_string_buffer(cap)
+    n = ctypes.c_uint64()
+    _check(load().kp_py_repr(_ptr(x), ctypes.c_uint64(x.size), buf, ctypes.c_uint64(cap), ctypes.byref(n)))
+    return buf.raw[:n.value].decode("ascii").split("\n")[:-1]
+
+
+def format_long_rows(kmers, c_neg, c_pos, pid, tails):
+    """The -l output rows (kp_format_long_rows): ``kmers`` uint8 ``[n, k]`` letters,
+    ``c_neg``/``c_pos`` int64 ``[n]``, ``pid`` ``[n]`` = index into ``tails`` (list of
+    str, each " pattern p_neg p_pos p_rate\n").  Returns the text as bytes; a row with no
+    counts raises ZeroDivisionError, as the reference's formula does."""
+    kmers = np.ascontiguousarray(kmers, dtype=np.uint8)
+    n, k = kmers.shape
+    c_neg = np.ascontiguousarray(c_neg, dtype=np.int64)
+    c_pos = np.ascontiguousarray(c_pos, dtype=np.int64)
+    pid = np.ascontiguousarray(pid, dtype=np.uint32)
+    tb = [t.encode("ascii") for t in tails]
+    off = np.zeros(len(tb) + 1, np.uint64)
+    off[1:] = np.cumsum([len(t) for t in tb])
+    tail_bytes = b"".join(tb) or b"\0"
+    lens = np.array([len(t) for t in tb] or [0], np.int64)
+    cap = int(n * (k + 3 * 32) + (lens[pid].sum() if n else 0)) + 1
+    out = np.empty(cap, np.uint8)  # (not zeroed: only the w bytes written are returned)
+    w = ctypes.c_uint64()
+    rc = load().kp_format_long_rows(kmers.ctypes.data_as(ctypes.c_void_p), int(k), _ptr(c_neg), _ptr(c_pos),
+                                    _ptr(pid), ctypes.c_uint64(n), tail_bytes, _ptr(off), ctypes.c_uint64(len(tb)),
+                                    _ptr(out), ctypes.c_uint64(cap), ctypes.byref(w))
+    if rc != 0:
+        msg = load().kp_last_error().decode(errors="replace")
+        if "division by zero" in msg:
+            raise ZeroDivisionError("float division by zero")
+        raise KPError(rc, msg)
+    return out[:w.value].tobytes()
 
 
 def device_count():

@@ -268,6 +268,32 @@ class KmerCounts(Mapping):
         sub = KmerCounts(self.k, codes, self.M[idx], self.U[idx])
         return sub._key_list(), sub.M.tolist(), sub.U.tolist()
 
+    def partition_rows(self, patterns):
+        """Every k-mer of every pattern, as :meth:`match_rows` lists them (patterns in order,
+        each one's k-mers in :func:`matches` order), vectorised over all patterns at once.
+        Returns ``(codes, pid)``: the k-mers' 2-bit codes and each row's pattern index."""
+        P = len(patterns)
+        if P == 0:
+            return np.zeros(0, np.uint64), np.zeros(0, np.int64)
+        k = len(patterns[0])
+        raw = np.frombuffer("".join(patterns).encode("ascii"), np.uint8).reshape(P, k)
+        size = np.zeros(256, np.int64)
+        base = np.zeros((256, 4), np.uint64)
+        for c, nucs in _code.items():
+            size[ord(c)] = len(nucs)
+            base[ord(c), :len(nucs)] = ["ACGT".index(n) for n in nucs]
+        pid = np.arange(P, dtype=np.int64)
+        codes = np.zeros(P, np.uint64)
+        for i in range(k - 1, -1, -1):  # position 0 last = innermost = fastest
+            ch = raw[pid, i]
+            rep = size[ch]
+            start = np.cumsum(rep) - rep
+            pid = np.repeat(pid, rep)
+            codes = np.repeat(codes, rep)
+            j = np.arange(pid.size) - np.repeat(start, rep)
+            codes = codes + base[np.repeat(ch, rep), j] * np.uint64(4 ** (k - 1 - i))
+        return codes, pid
+
     def pattern_counts(self, patterns):
         """get_M_U (pattern_utils.py:192-215) for many patterns: summed (M, U) of the
         k-mers each pattern matches (every one must be in the table)."""

@@ -1,0 +1,76 @@
+"""The output writer (cli.write_partition; reference cli.py:301-316) on the host: the native
+-l row formatter (kp_format_long_rows) must write exactly the reference's f-string rows,
+floats as Python's repr()."""
+import io
+import itertools
+
+import numpy as np
+import pytest
+
+from kmerpapa_amd import engine
+from kmerpapa_amd.cli import write_partition
+from tests.fixtures import context_table
+
+
+def test_py_repr_matches_python():
+    rng = np.random.RandomState(7)
+    xs = np.concatenate([rng.rand(100000), rng.rand(50000) * 1e-5, 10.0 ** rng.uniform(-320, 308, 50000),
+                         rng.randint(0, 10 ** 6, 50000) / rng.randint(1, 10 ** 7, 50000),
+                         [0.0, -0.0, 1.0, 1e16, 1e15, 1.2345678901234568e17, 1e-4, 1e-5, 1.234e-4, 1.5e-7,
+                          np.inf, -np.inf, np.nan, 5e-324, 1.7976931348623157e308, 0.1, 0.5,
+                          9999999999999998.0, 1234567890123456.7, -2.5e-300]])
+    got = engine.py_repr(xs)
+    assert got == [repr(float(x)) for x in xs]
+
+
+def _reference_rows(out, names, counts, table, alpha, beta):
+    """cli.py:301-316 as the reference writes -l rows (Python f-strings, matches() order)."""
+    from kmerpapa_amd.pattern_utils import matches
+    print("context", "c_neg", "c_pos", "c_rate", "pattern", "p_neg", "p_pos", "p_rate", file=out)
+    for pat, (Mp, Up) in zip(names, counts):
+        p = (Mp + alpha) / (Mp + Up + alpha + beta)
+        for context in matches(pat):
+            nm, ns = table[context]
+            print(context, ns, nm, float(nm) / (nm + ns), pat, Up, Mp, p, file=out)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_long_output_rows_equal_reference_formula(seed):
+    ctx, gp, nm, nu = context_table(5)
+    from kmerpapa_amd.io_utils import KmerCounts
+    keys = sorted(ctx)
+    codes = np.array([int("".join(str("ACGT".index(c)) for c in k), 4) for k in keys], np.uint64)
+    table = KmerCounts(5, codes, [ctx[k][0] for k in keys], [ctx[k][1] for k in keys])
+    # a random partition of NNMNN: split positions until patterns are small
+    rng = np.random.RandomState(seed)
+    split = {"N": [("R", "Y"), ("S", "W"), ("K", "M")], "M": [("A", "C")], "R": [("A", "G")], "Y": [("C", "T")],
+             "S": [("C", "G")], "W": [("A", "T")], "K": [("G", "T")]}
+    names, todo = [], [gp]
+    while todo:
+        pat = todo.pop()
+        amb = [i for i, c in enumerate(pat) if c in split]
+        if not amb or rng.rand() < 0.15:
+            names.append(pat)
+            continue
+        i = amb[rng.randint(len(amb))]
+        a, b = split[pat[i]][rng.randint(len(split[pat[i]]))]
+        todo += [pat[:i] + a + pat[i + 1:], pat[:i] + b + pat[i + 1:]]
+    counts = table.pattern_counts(names)
+    assert sum(c[0] for c in counts) == nm
+    alpha, beta = 0.5, 31.7
+    got, ref = io.StringIO(), io.StringIO()
+    write_partition(got, names, counts, table, alpha, beta, True)
+    _reference_rows(ref, names, counts, table, alpha, beta)
+    assert got.getvalue() == ref.getvalue()
+    short = io.StringIO()
+    write_partition(short, names, counts, table, alpha, beta, False)
+    assert short.getvalue().count("\n") == len(names) + 1
+
+
+def test_long_output_zero_counts_raise_like_reference():
+    from kmerpapa_amd.io_utils import KmerCounts
+    codes = np.array([0, 1, 2, 3], np.uint64)
+    table = KmerCounts(1, codes, [1, 0, 2, 3], [5, 0, 7, 9])
+    with pytest.raises(ZeroDivisionError):
+        write_partition(io.StringIO(), ["N"], [(6, 21)], table, 0.5, 1.0, True)
+    assert list(itertools.islice(engine.py_repr([0.25]), 1)) == ["0.25"]

@@ -10,6 +10,9 @@
 //         trim    the same, with hipMemPoolTrimTo(pool, 0) after every free
 //         own     an explicitly created pool (hipMemPoolCreate)
 //         malloc  hipMalloc / hipFree (control)
+//         sleep   the default pool, waiting 12 s after every free (time for the driver to
+//                 finish clearing the freed memory) before the next allocation
+// argv[2] = largest size in GB (default 200)
 // An allocation that fails ends the sequence cleanly (everything outstanding is freed
 // before the process exits: the round-2 version called exit(1) with a pool block live,
 // and the runtime's teardown then aborted with "double free").
@@ -18,6 +21,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 __device__ __host__ inline uint32_t pat(size_t i, uint32_t seed) { return (uint32_t)(i * 2654435761u) ^ seed; }
 
@@ -72,6 +76,7 @@ static void pool_attrs(hipMemPool_t pool, const char *tag) {
 int main(int argc, char **argv) {
     const char *mode = argc > 1 ? argv[1] : "pool";
     const bool use_pool = strcmp(mode, "malloc") != 0;
+    const double max_gb = argc > 2 ? atof(argv[2]) : 200.0;
     const double gbs[] = {8, 100, 140, 150, 200};
     hipStream_t s = nullptr;
     if (!ok(hipStreamCreate(&s), "hipStreamCreate")) return 1;
@@ -91,6 +96,7 @@ int main(int argc, char **argv) {
     uint32_t prev = 0;
     int a = 0;
     for (double gb : gbs) {
+        if (gb > max_gb) break;
         ++a;
         const uint32_t seed = 0x9e3779b9u * (uint32_t)a;
         const size_t bytes = (size_t)(gb * 1e9) & ~(size_t)4095, n = bytes / 4;
@@ -132,6 +138,7 @@ int main(int argc, char **argv) {
         if (!ok(e, "free")) break;
         if (strcmp(mode, "trim") == 0 && !ok(hipMemPoolTrimTo(pool, 0), "trim")) break;
         pool_attrs(pool, "after free");
+        if (strcmp(mode, "sleep") == 0) sleep(12);
         prev = seed;
         if (!good) break;
     }

@@ -1,6 +1,8 @@
 """End-to-end CLI run on the benchmark's synthetic 9-mer counts (BASELINE configs[3]):
 writes positive/background count files, then times `python -m kmerpapa_amd` exactly as a
-user would run it (grid CV + final fit + output table).  Prints one JSON line."""
+user would run it (grid CV + final fit + output table).  Prints one JSON line.
+usage: cli_9mer.py [OUTDIR [CLI ARGS...]]: CLI ARGS replace the default grid CV arguments
+(e.g. "-c 5 -a 2 -l": one fit with the long output)."""
 import json
 import os
 import subprocess
@@ -19,9 +21,10 @@ with open(os.path.join(out, "pos.txt"), "w") as f:
     f.writelines(f"{k} {m}\n" for k, m in zip(kmers, M))
 with open(os.path.join(out, "bg.txt"), "w") as f:
     f.writelines(f"{k} {m + u}\n" for k, m, u in zip(kmers, M, U))
+grid = sys.argv[2:] or ["-c", "3", "4", "5", "6", "7", "-a", "0.5", "1", "2", "5", "10", "--nfolds", "5", "--seed", "1",
+                        "-f", os.path.join(out, "cv.txt")]
 cmd = [sys.executable, "-m", "kmerpapa_amd", "-p", os.path.join(out, "pos.txt"), "-b", os.path.join(out, "bg.txt"),
-       "-c", "3", "4", "5", "6", "7", "-a", "0.5", "1", "2", "5", "10", "--nfolds", "5", "--seed", "1",
-       "-o", os.path.join(out, "partition.txt"), "-f", os.path.join(out, "cv.txt")]
+       "-o", os.path.join(out, "partition.txt")] + grid
 metrics = os.path.join(out, "metrics.jsonl")
 if os.path.exists(metrics):
     os.remove(metrics)
