@@ -118,6 +118,10 @@ int kp_counts_fold(kp_plan *plan, int fold, const void *M_fold, const void *U_fo
 int kp_pass(kp_plan *plan, const kp_group *groups, int n_groups, float *root_train, float *root_test,
             uint64_t *n_leaves);
 int kp_last_pass_stats(const kp_plan *plan, kp_pass_stats *out);
+/* Tuning: with KP_LAUNCH_TIMES=1 in the environment, the device time (ms) of every sweep
+ * launch of the last pass (lane classes in order, high levels ascending); *n = launches
+ * (0 without the variable), at most cap written to ms. */
+int kp_last_launch_ms(const kp_plan *plan, float *ms, int cap, int *n);
 
 /* Allocate the per-lane device buffers (score rows, backtrack nodes) for `lanes` lanes now,
  * so that later passes of up to that many lanes allocate nothing.  Buffers only grow.

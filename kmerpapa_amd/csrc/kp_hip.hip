@@ -431,6 +431,8 @@ struct kp_plan {
     std::vector<kp_group_dev> last_groups;  // device groups of the last pass (dump)
     std::vector<uint32_t> last_lanegrp;
     kp_pass_stats stats{};
+    std::vector<hipEvent_t> lev;     // per-launch events (KP_LAUNCH_TIMES=1)
+    std::vector<float> launch_ms;    // per-launch times of the last pass (class-major, H ascending)
 };
 
 static void free_scores(kp_plan *p);  // the score rows (pool or hipMalloc), defined below
@@ -565,6 +567,7 @@ void kp_plan_destroy(kp_plan *p) {
                     p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
                     p->d_leaves};
     for (void *b : bufs) dfree(b);
+    for (hipEvent_t e : p->lev) (void)hipEventDestroy(e);
     delete p;
 }
 
@@ -962,10 +965,24 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     // (default 3) are read non-temporally: under that order they are not re-read while
     // still in the Infinity Cache, so they no longer evict the rows of the fast positions
     // that are (9-mer pass 403-408 -> 397-398 ms; 2: 399-400, 4: 417)
+    // KP_NT_SLOW_H = comma list: a count per high level (launch), for per-launch tuning;
+    // levels past the list (or without it) take KP_NT_SLOW
+    std::vector<uint32_t> ntmask_h(hp.hmax + 1, 0);
     {
         const int nslow = getenv("KP_NT_SLOW") ? atoi(getenv("KP_NT_SLOW")) : 3;
-        P.ntmask = 0;
-        for (int q = 0; q < nslow && q < (int)hp.perm.size(); ++q) P.ntmask |= 1u << hp.perm[hp.perm.size() - 1 - q];
+        std::vector<int> per(hp.hmax + 1, nslow);
+        if (const char *e = getenv("KP_NT_SLOW_H")) {
+            int H = 0;
+            for (const char *q = e; *q && H <= hp.hmax; ++H) {
+                per[H] = atoi(q);
+                while (*q && *q != ',') ++q;
+                if (*q == ',') ++q;
+            }
+        }
+        for (int H = 0; H <= hp.hmax; ++H)
+            for (int q = 0; q < per[H] && q < (int)hp.perm.size(); ++q)
+                ntmask_h[H] |= 1u << hp.perm[hp.perm.size() - 1 - q];
+        P.ntmask = ntmask_h[0];
     }
     P.stamps = nullptr;
 #ifdef KP_STAMPS
@@ -992,6 +1009,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
             KP_HIP(hipStreamWaitEvent(c->side[q - 1], c->ev[3], 0));
     }
     uint64_t launches = 0;
+    // KP_LAUNCH_TIMES=1: HIP events around every launch (kp_last_launch_ms; tuning only)
+    const bool timed = getenv("KP_LAUNCH_TIMES") && atoi(getenv("KP_LAUNCH_TIMES")) == 1;
     for (size_t q = 0; q < classes.size(); ++q) {
         const hipStream_t st = (multi && q > 0) ? c->side[(q - 1) % KP_SIDE_STREAMS] : c->stream;
         const size_t i = classes[q].first, j = classes[q].second;
@@ -1002,13 +1021,23 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
             Q.hbase = hp.hoff[H];
             Q.H = H;
             Q.groups = p->d_groups + i;
+            Q.ntmask = ntmask_h[H];
             size_t lds = dp_lds_bytes(hp, dg[i].nl, sizeof(CT));
 #ifdef KP_ABLATION
             // ablation build only: extra LDS per workgroup to force lower occupancy
             if (getenv("KP_LDS_PAD")) lds += (size_t)atol(getenv("KP_LDS_PAD"));
 #endif
+            if (timed) {
+                while (p->lev.size() < 2 * (launches + 1)) {
+                    hipEvent_t e;
+                    KP_HIP(hipEventCreate(&e));
+                    p->lev.push_back(e);
+                }
+                KP_HIP(hipEventRecord(p->lev[2 * launches], st));
+            }
             int rc = launch_dp_nl<CT>(dg[i].nl, st, Q, (unsigned)nb, (unsigned)(j - i), threads, lds);
             if (rc) return rc;
+            if (timed) KP_HIP(hipEventRecord(p->lev[2 * launches + 1], st));
             ++launches;
         }
     }
@@ -1078,6 +1107,13 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     }
 #endif
     KP_HIP(hipEventElapsedTime(&bt_ms, c->ev[1], c->ev[2]));
+    p->launch_ms.clear();
+    if (timed)
+        for (uint64_t q = 0; q < launches; ++q) {
+            float ms = 0;
+            KP_HIP(hipEventElapsedTime(&ms, p->lev[2 * q], p->lev[2 * q + 1]));
+            p->launch_ms.push_back(ms);
+        }
     if (P.dbg) {  // ablation build: timings only, never numbers
         p->stats.dp_ms = dp_ms;
         p->stats.backtrack_ms = 0;
@@ -1154,6 +1190,13 @@ int kp_reserve_lanes(kp_plan *p, uint32_t lanes) {
         KP_HIP(hipMemsetAsync(p->d_S, 0, p->hp.g.nblocks * (size_t)p->lanes_cap * p->hp.g.Bpad * 4, p->ctx->stream));
         KP_HIP(hipStreamSynchronize(p->ctx->stream));
     }
+    return KP_OK;
+}
+
+int kp_last_launch_ms(const kp_plan *p, float *ms, int cap, int *n) {
+    if (!p || !n || (cap > 0 && !ms)) return fail(KP_E_ARG, "null argument");
+    *n = (int)p->launch_ms.size();
+    for (int i = 0; i < cap && i < *n; ++i) ms[i] = p->launch_ms[i];
     return KP_OK;
 }
 

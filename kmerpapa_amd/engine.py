@@ -60,7 +60,7 @@ class KPPassStats(ctypes.Structure):
 
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
            "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
-           "kp_reserve_lanes", "kp_last_pass_stats", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
+           "kp_reserve_lanes", "kp_last_pass_stats", "kp_last_launch_ms", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
            "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free",
            "kp_format_long_rows", "kp_py_repr"]
 
@@ -99,6 +99,7 @@ def load():
         L.kp_counts_fold.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_uint64]
         L.kp_pass.argtypes = [vp, ctypes.POINTER(KPGroup), ctypes.c_int, vp, vp, vp]
         L.kp_last_pass_stats.argtypes = [vp, ctypes.POINTER(KPPassStats)]
+        L.kp_last_launch_ms.argtypes = [vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.kp_reserve_lanes.argtypes = [vp, ctypes.c_uint32]
         L.kp_fit_leaves.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u64p]
         L.kp_dump_lane.argtypes = [vp, ctypes.c_uint32, vp, vp]
@@ -133,7 +134,7 @@ def _ptr(a):
 # launch knobs read by kp_hip.hip (every setting gives the same scores; they change timing)
 LAUNCH_KNOBS = ("KP_DP_THREADS", "KP_LANES_PER_WG", "KP_XCD_REMAP", "KP_LANE_SPLIT", "KP_NT_STORE", "KP_NT_SLOW",
                 "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER", "KP_EXACT_LOGS",
-               "KP_CLASS_STREAMS")
+               "KP_CLASS_STREAMS", "KP_NT_SLOW_H")
 
 
 _toolchain = None
@@ -422,6 +423,14 @@ class Plan:
         s = KPPassStats()
         _check(load().kp_last_pass_stats(self._h, ctypes.byref(s)))
         return {name: getattr(s, name) for name, _ in KPPassStats._fields_}
+
+    def launch_ms(self):
+        """Per-launch device times (ms) of the last pass (needs KP_LAUNCH_TIMES=1)."""
+        n = ctypes.c_int()
+        _check(load().kp_last_launch_ms(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, np.float32)
+        _check(load().kp_last_launch_ms(self._h, _ptr(out), n.value, ctypes.byref(n)))
+        return out
 
     def leaves(self, lane):
         """Cell indices of the optimal partition of ``lane``, in backtrack order."""
