@@ -567,11 +567,19 @@ def materialize(M, U, groups):
     return M, U, groups
 
 
+# lanes a pass may hold when it packs groups of different widths (KMERPAPA_PASS_LANES)
+PASS_LANES = int(os.environ.get("KMERPAPA_PASS_LANES", "7"))
+
+
 def pass_cap(groups, fit):
-    """Lanes per pass: the largest group, if it fits.  Passes with more lanes are not faster
-    per lane (each (alpha, fold) group is its own set of workgroups), but need more HBM,
-    and a large allocation can be slow (freed HBM is wiped before reuse)."""
-    return min(fit, max([len(g[3]) for g in groups] or [1]))
+    """Lanes per pass: up to PASS_LANES (7), or the largest group if wider, if that fits.
+    Groups of one pass that differ in width run as concurrent lane classes on their own
+    HIP streams (kp_hip.hip run_pass), so a small group packed beside a full one costs less
+    than alone: 9-mer passes of 4+2 lanes 531 ms against 339 + 222 sequential, 5+1 529
+    against 394 + 144; two 5-lane groups (10 lanes) never share a pass: passes of equal
+    full groups are not faster per lane and would need more HBM."""
+    widest = max([len(g[3]) for g in groups] or [1])
+    return min(fit, max(PASS_LANES, widest))
 
 
 def pack_passes(groups, max_lanes):

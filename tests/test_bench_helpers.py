@@ -1,6 +1,6 @@
 """bench.py's host-side helpers (no GPU): the synthetic count table is the CLI's sorted
 array table, the 8-rank CV shares cover every (alpha, fold, penalty) lane exactly once in
-lane order, and passes never exceed one group's lanes."""
+lane order, and passes never exceed the pass cap."""
 import numpy as np
 
 import bench
@@ -35,11 +35,15 @@ def test_cv_shares_cover_every_lane_once():
         assert max(lanes) - min(lanes) <= 1
 
 
-def test_pass_cap_is_largest_group_if_it_fits():
+def test_pass_cap_packs_small_groups_beside_full_ones():
     groups = [(0, 1.0, 1.0, [1.0] * 5), (1, 1.0, 1.0, [1.0] * 3)]
-    assert engine.pass_cap(groups, 9) == 5
+    assert engine.pass_cap(groups, 9) == engine.PASS_LANES == 7
     assert engine.pass_cap(groups, 4) == 4
-    assert engine.pass_cap([], 9) == 1
+    assert engine.pass_cap([(0, 1.0, 1.0, [1.0] * 8)], 9) == 8
+    assert engine.pass_cap([], 9) == min(9, engine.PASS_LANES)
+    # an 8-rank share of the 5x5x5 grid: [5, 5, 5, 1] -> passes [5], [5], [5, 1]
+    share = [(f, 1.0, 1.0, [1.0] * n) for f, n in enumerate([5, 5, 5, 1])]
+    assert [[len(g[3]) for g in p] for p in engine.pack_passes(share, engine.pass_cap(share, 9))] == [[5], [5], [5, 1]]
 
 
 def test_host_cores_positive():

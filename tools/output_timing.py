@@ -14,6 +14,24 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from kmerpapa_amd.cli import write_partition  # noqa: E402
 
+
+def reference_writer(out, names, counts, table, alpha, beta, long_output):
+    """The round-2 writer: the reference's f-string per row (cli.py:301-316), k-mers of each
+    pattern from one numpy enumeration per pattern (KmerCounts.match_rows)."""
+    if long_output:
+        print("context", "c_neg", "c_pos", "c_rate", "pattern", "p_neg", "p_pos", "p_rate", file=out)
+    else:
+        print("pattern", "p_neg", "p_pos", "p_rate", file=out)
+    for pat, (Mp, Up) in zip(names, counts):
+        p = (Mp + alpha) / (Mp + Up + alpha + beta)
+        if long_output:
+            tail = f" {pat} {Up} {Mp} {p}\n"
+            rows = table.match_rows(pat)
+            out.write("".join(f"{context} {ns} {nm} {float(nm) / (nm + ns)}{tail}" for context, nm, ns in zip(*rows)))
+        else:
+            print(pat, Up, Mp, p, file=out)
+
+
 kmers, M, U = bench.synthetic_counts("NNNNMNNNN")
 table = bench.kmer_table(kmers, M, U)
 nm, nu = int(M.sum()), int(U.sum())
@@ -30,10 +48,15 @@ for n, names in parts.items():
     counts = table.pattern_counts(names)
     assert sum(c[0] for c in counts) == nm and sum(c[1] for c in counts) == nu
     for long_output in (False, True):
-        buf = io.StringIO()
-        t0 = time.perf_counter()
-        write_partition(buf, names, counts, table, alpha, beta, long_output)
-        dt = time.perf_counter() - t0
-        text = buf.getvalue()
-        print(json.dumps({"patterns": len(names), "long": long_output, "rows": text.count("\n") - 1,
-                          "seconds": round(dt, 4), "md5": hashlib.md5(text.encode()).hexdigest()}), flush=True)
+        for name, fn in (("native", write_partition), ("reference_fstring", reference_writer)):
+            fn(io.StringIO(), names, counts, table, alpha, beta, long_output)  # warm
+            with open(os.devnull, "w") as null:  # to a real file object, as the CLI writes
+                t0 = time.perf_counter()
+                fn(null, names, counts, table, alpha, beta, long_output)
+                dt = time.perf_counter() - t0
+            buf = io.StringIO()
+            fn(buf, names, counts, table, alpha, beta, long_output)
+            text = buf.getvalue()
+            print(json.dumps({"writer": name, "patterns": len(names), "long": long_output,
+                              "rows": text.count("\n") - 1, "seconds": round(dt, 4),
+                              "md5": hashlib.md5(text.encode()).hexdigest()}), flush=True)
