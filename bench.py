@@ -297,10 +297,7 @@ def cv_run(plan, prep, gen_pat, groups):
 def shadow_host_side(prep, gen_pat, device):
     """The host work every rank of a multi-GPU job does before and beside its passes (cv_run
     without the passes): the plan's table build and upload, the all-data counts in k-mer
-    order and the whole fold split drawn fold by fold.  Run by the N - 1 other "ranks" of a
-    modelled world while one rank's share runs for real, so that share sees the host
-    contention of N concurrent ranks (threads of one process: they also share one GIL,
-    which makes the model pessimistic against N separate processes)."""
+    order and the whole fold split drawn fold by fold."""
     from kmerpapa_amd.CV_tools import all_counts, fold_stream
     nf, itype = prep["nfolds"], prep["itype"]
     p = engine.Plan(device, gen_pat, 0)
@@ -315,28 +312,74 @@ def shadow_host_side(prep, gen_pat, device):
     p.close()
 
 
-def model_world(plan, prep, gen_pat, world):
+def shadow_main(config, gen_pat):
+    """``bench.py --shadow``: a stand-in for another rank's process.  Prepares the same
+    counts, says "ready", then runs shadow_host_side once per "go" line on stdin, answering
+    "done SECONDS"; exits on EOF."""
+    cfg = dict(CONFIGS[config])
+    prep = prepare(gen_pat, alphas=cfg["alphas"], penalties=cfg["penalties"], nfolds=cfg["nfolds"])
+    dev = engine.get_device(0)
+    print("ready", flush=True)
+    for line in sys.stdin:
+        if line.strip() != "go":
+            continue
+        t0 = time.perf_counter()
+        shadow_host_side(prep, gen_pat, dev)
+        print(f"done {time.perf_counter() - t0:.4f}", flush=True)
+
+
+class Shadows:
+    """Pool of shadow rank processes (``bench.py --shadow``), one Python process each -- as
+    the ranks of a real job are -- so the modelled rank sees N concurrent host sides with
+    their own interpreters and GILs."""
+
+    def __init__(self, n, config, gen_pat):
+        import subprocess
+        self.procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__), "--shadow", "--config", config,
+                                        "--pattern", gen_pat], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
+                                       text=True, cwd=ROOT) for _ in range(n)]
+        for p in self.procs:
+            if p.stdout.readline().strip() != "ready":
+                raise RuntimeError("shadow rank failed to start")
+
+    def go(self, n):
+        for p in self.procs[:n]:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+
+    def wait(self, n):
+        out = []
+        for p in self.procs[:n]:
+            line = p.stdout.readline().split()
+            if not line or line[0] != "done":
+                raise RuntimeError("shadow rank failed")
+            out.append(float(line[1]))
+        return out
+
+    def close(self):
+        for p in self.procs:
+            p.stdin.close()
+            p.wait(timeout=60)
+
+
+def model_world(plan, prep, gen_pat, world, shadows):
     """Modelled wall-clock of the full CV on ``world`` GPUs: every rank's lane-granular share
     (shard.rank_groups) is run as that rank runs it (cv_run: its own pipelined fold split,
     table build and passes), one share after the other on this GPU, each while world - 1
-    shadow threads do the other ranks' host side at the same time (shadow_host_side).  Only
-    the GPU part is serialised; there is no data-path collective, so the
-    job's wall-clock is the slowest share."""
-    import threading
+    shadow rank processes do the other ranks' host side at the same time
+    (shadow_host_side).  Only the GPU part is serialised; there is no data-path collective
+    (SURVEY.md 8e), so the job's wall-clock is the slowest share."""
     from kmerpapa_amd.shard import rank_groups
-    shares = []
+    shares, shadow_s = [], []
     for r in range(world):
-        shadows = [threading.Thread(target=shadow_host_side, args=(prep, gen_pat, plan.device))
-                   for _ in range(world - 1)]
-        for th in shadows:
-            th.start()
+        shadows.go(world - 1)
         shares.append(cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], r, world)))
-        for th in shadows:
-            th.join()
+        shadow_s += shadows.wait(world - 1)
     return {"world": world, "share_s": [round(x["wall_s"], 4) for x in shares],
             "share_lanes": [x["lanes"] for x in shares],
             "share_passes_start_s": [round(x["passes_start_s"], 4) for x in shares],
             "share_fold_split_s": [round(x["fold_split_s"], 4) for x in shares],
+            "shadow_host_side_s": [round(min(shadow_s), 4), round(max(shadow_s), 4)] if shadow_s else None,
             "wall_s": max(x["wall_s"] for x in shares)}
 
 
@@ -351,12 +394,16 @@ def full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds=(2, 4, 8)):
     out = cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], rank, world))
     out["hbm_alloc_s"] = prep["t_alloc"]
     out["wall_s_incl_alloc"] = out["wall_s"] + prep["t_alloc"]
-    if world == 1:
+    if world == 1 and model_worlds:
         out["models"] = {}
-        for w in model_worlds:
-            m = model_world(plan, prep, gen_pat, w)
-            m["speedup"] = out["wall_s"] / m["wall_s"]
-            out["models"][str(w)] = m
+        shadows = Shadows(max(model_worlds) - 1, prep["config"], gen_pat)
+        try:
+            for w in model_worlds:
+                m = model_world(plan, prep, gen_pat, w, shadows)
+                m["speedup"] = out["wall_s"] / m["wall_s"]
+                out["models"][str(w)] = m
+        finally:
+            shadows.close()
     return out
 
 
@@ -371,7 +418,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--max-block", type=int, default=0)
     ap.add_argument("--no-full-cv", action="store_true", help="skip the full grid CV wall-clock leg")
+    ap.add_argument("--model-worlds", default="2,4,8",
+                    help="GPU counts whose full-CV wall-clock is modelled at N=1 (comma list, empty = none)")
+    ap.add_argument("--shadow", action="store_true", help=argparse.SUPPRESS)  # a modelled rank's host side
     a = ap.parse_args()
+    if a.shadow:
+        return shadow_main(a.config, a.pattern or CONFIGS[a.config]["gen_pat"])
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -386,6 +438,7 @@ def main():
         cfg["gen_pat"] = a.pattern
     gen_pat = cfg["gen_pat"]
     prep = prepare(gen_pat, alphas=cfg["alphas"], penalties=cfg["penalties"], nfolds=cfg["nfolds"])
+    prep["config"] = a.config
     ndev = engine.device_count()
     prep["device"] = local % max(1, ndev)  # one GPU per rank (several ranks per GPU only in rehearsals)
     groups = prep["groups"]
@@ -406,7 +459,8 @@ def main():
     plan = engine.get_plan(prep["device"], gen_pat, a.max_block)
     prep["t_plan"] = time.perf_counter() - t0
     cap = engine.pass_cap(groups, plan.lanes_that_fit())
-    worlds = () if a.no_full_cv else ((world, 2, 4, 8) if world == 1 else (world,))
+    model_worlds = tuple(int(x) for x in a.model_worlds.split(",") if x.strip())
+    worlds = () if a.no_full_cv else ((world,) + model_worlds if world == 1 else (world,))
     most = max([len(groups[0][3])] + [sum(len(g[3]) for g in p) for w in worlds
                                       for passes in cv_shares(prep, w, cap) for p in passes])
     t0 = time.perf_counter()
@@ -434,7 +488,7 @@ def main():
     cv = None
     if not a.no_full_cv:
         barrier()
-        cv = full_cv(plan, prep, gen_pat, rank, world, cap)
+        cv = full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds)
         cv["wall_s"] = max_over_ranks(cv["wall_s"])
 
     units_rank = sum(s["units"] for s in stats)

@@ -370,12 +370,12 @@ __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint3
 
 // min over one 4-pair chunk of a cell's split-pair list (c1 | c2 << 16 per pair, kp_plan.h
 // lpairs) for W lanes from j0; all 8*W LDS reads issue before the first min
-template <int NL, int W, typename SP>
+template <int NL, int W, int NPC = 4, typename SP>
 __host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0, float *lmin) {
     const uint32_t e[4] = {c.x, c.y, c.z, c.w};
     float va[4][W], vb[4][W];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
+    for (int p = 0; p < NPC; ++p) {
         const uint32_t c1 = e[p] & 0xFFFFu, c2 = e[p] >> 16;
 #pragma unroll
         for (int j = 0; j < W; ++j) {
@@ -384,7 +384,7 @@ __host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0,
         }
     }
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < NPC; ++p)
 #pragma unroll
         for (int j = 0; j < W; ++j) lmin[j] = fminf(lmin[j], va[p][j] + vb[p][j]);
 }
@@ -408,10 +408,23 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
     float lmin[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) lmin[j] = row[j];
+#ifdef KP_HALF_CHUNKS
+    // a chunk whose last two pairs are padding runs as a 2-pair chunk
+#pragma unroll
+    for (int k = 0; k < KP_PRE_CHUNKS; ++k)
+        if (4u * k < npairs) {
+            if (npairs - 4u * k > 2u)
+                kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
+            else
+                kp_chunk_minv<NL, W, 2>(st, pre[k], j0, lmin);
+        }
+    for (uint32_t k = KP_PRE_CHUNKS; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+#else
 #pragma unroll
     for (int k = 0; k < KP_PRE_CHUNKS; ++k)
         if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
     for (uint32_t k = KP_PRE_CHUNKS; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+#endif
     kp_cell_store<W>(row, lmin, sc, pen, alpha, beta);
 }
 

@@ -8,6 +8,7 @@ import itertools
 import json
 import os
 import sys
+import tempfile
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -50,10 +51,13 @@ for n, names in parts.items():
     for long_output in (False, True):
         for name, fn in (("native", write_partition), ("reference_fstring", reference_writer)):
             fn(io.StringIO(), names, counts, table, alpha, beta, long_output)  # warm
-            with open(os.devnull, "w") as null:  # to a real file object, as the CLI writes
+            path = os.path.join(tempfile.gettempdir(), f"kp_out_{os.getpid()}.txt")
+            with open(path, "w") as fh:  # a real file, as the CLI's -o writes
                 t0 = time.perf_counter()
-                fn(null, names, counts, table, alpha, beta, long_output)
+                fn(fh, names, counts, table, alpha, beta, long_output)
+                fh.flush()
                 dt = time.perf_counter() - t0
+            os.remove(path)
             buf = io.StringIO()
             fn(buf, names, counts, table, alpha, beta, long_output)
             text = buf.getvalue()
