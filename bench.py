@@ -294,14 +294,16 @@ def cv_run(plan, prep, gen_pat, groups):
             "fold_split_s": box["t_fold"][-1], "passes_start_s": t_start, "lanes": sum(len(g[3]) for g in groups)}
 
 
-def shadow_host_side(prep, gen_pat, device):
+def shadow_host_side(prep, gen_pat):
     """The host work every rank of a multi-GPU job does before and beside its passes (cv_run
-    without the passes): the plan's table build and upload, the all-data counts in k-mer
-    order and the whole fold split drawn fold by fold."""
+    without the passes): the plan's host-side table build, the all-data counts in k-mer
+    order and the whole fold split drawn fold by fold.  No GPU: a shadow rank must not hold
+    a context on the GPU the modelled rank measures on (other processes' contexts and
+    queues on the same device slowed its passes ~2x), while a real rank has a GPU of its
+    own."""
     from kmerpapa_amd.CV_tools import all_counts, fold_stream
     nf, itype = prep["nfolds"], prep["itype"]
-    p = engine.Plan(device, gen_pat, 0)
-    nk = p.info["n_kmers"]
+    nk = engine.plan_info(gen_pat)["n_kmers"]
     contexts, Ma, Ua = all_counts(prep["ctx"], itype)
     idx = engine.kmer_order(gen_pat, contexts)
     M_all = np.zeros(nk, itype)
@@ -309,7 +311,6 @@ def shadow_host_side(prep, gen_pat, device):
     for f, Mf, Uf in fold_stream(prep["ctx"], nf, np.random.RandomState(1), itype):
         mk = np.zeros(nk, itype)
         mk[idx] = Mf
-    p.close()
 
 
 def shadow_main(config, gen_pat):
@@ -318,13 +319,12 @@ def shadow_main(config, gen_pat):
     "done SECONDS"; exits on EOF."""
     cfg = dict(CONFIGS[config])
     prep = prepare(gen_pat, alphas=cfg["alphas"], penalties=cfg["penalties"], nfolds=cfg["nfolds"])
-    dev = engine.get_device(0)
     print("ready", flush=True)
     for line in sys.stdin:
         if line.strip() != "go":
             continue
         t0 = time.perf_counter()
-        shadow_host_side(prep, gen_pat, dev)
+        shadow_host_side(prep, gen_pat)
         print(f"done {time.perf_counter() - t0:.4f}", flush=True)
 
 

@@ -96,6 +96,9 @@ int kp_device_mem(kp_ctx *ctx, uint64_t *free_bytes, uint64_t *total_bytes);
 int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan **out);
 void kp_plan_destroy(kp_plan *plan);
 int kp_plan_get_info(const kp_plan *plan, kp_plan_info *out);
+/* Host-only (no GPU): build the plan's tables on the host and report their info -- the
+ * lattice size and device bytes per lane a job would need, before any device is touched. */
+int kp_plan_host(const char *gen_pat, uint32_t max_block, kp_plan_info *out);
 
 /* Upload fold counts of every k-mer: M, U are [n_kmers][nf] arrays of itype_bytes (4 or
  * 8) unsigned integers, k-mers in KmerEnumeration order (position 0 fastest, nucleotide

@@ -571,9 +571,7 @@ void kp_plan_destroy(kp_plan *p) {
     delete p;
 }
 
-int kp_plan_get_info(const kp_plan *p, kp_plan_info *o) {
-    if (!p || !o) return fail(KP_E_ARG, "null argument");
-    const kp::host_plan &h = p->hp;
+static void info_of(const kp::host_plan &h, kp_plan_info *o) {
     o->npat = h.npat;
     o->nblocks = h.g.nblocks;
     o->n_kmers = h.n_kmers;
@@ -588,6 +586,20 @@ int kp_plan_get_info(const kp_plan *p, kp_plan_info *o) {
     // train scores + backtrack node pool + leaf list
     o->bytes_per_lane = h.g.nblocks * (uint64_t)h.g.Bpad * 4 + (uint64_t)node_cap_of(h) * sizeof(kp_node) +
                         h.n_kmers * 8 + 4096;
+}
+
+int kp_plan_get_info(const kp_plan *p, kp_plan_info *o) {
+    if (!p || !o) return fail(KP_E_ARG, "null argument");
+    info_of(p->hp, o);
+    return KP_OK;
+}
+
+int kp_plan_host(const char *gen_pat, uint32_t max_block, kp_plan_info *o) {
+    if (!gen_pat || !o) return fail(KP_E_ARG, "null argument");
+    kp::host_plan hp;
+    std::string err = kp::build_plan(gen_pat, max_block ? max_block : 4096u, hp);
+    if (!err.empty()) return fail(KP_E_ARG, err);
+    info_of(hp, o);
     return KP_OK;
 }
 

@@ -59,7 +59,7 @@ class KPPassStats(ctypes.Structure):
 
 
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
-           "kp_plan_destroy", "kp_plan_get_info", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
+           "kp_plan_destroy", "kp_plan_get_info", "kp_plan_host", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
            "kp_reserve_lanes", "kp_last_pass_stats", "kp_last_launch_ms", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
            "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free",
            "kp_format_long_rows", "kp_py_repr"]
@@ -87,6 +87,7 @@ def load():
         L.kp_plan_destroy.argtypes = [vp]
         L.kp_plan_destroy.restype = None
         L.kp_plan_get_info.argtypes = [vp, ctypes.POINTER(KPPlanInfo)]
+        L.kp_plan_host.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(KPPlanInfo)]
         L.kp_kmer_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                     ctypes.POINTER(vp)]
         L.kp_kmer_table_info.argtypes = [vp, u64p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
@@ -282,6 +283,14 @@ def format_long_rows(kmers, c_neg, c_pos, pid, tails):
             raise ZeroDivisionError("float division by zero")
         raise KPError(rc, msg)
     return out[:w.value].tobytes()
+
+
+def plan_info(gen_pat, max_block=0):
+    """The plan's info (cells, blocks, device bytes per lane, ...) built on the host only
+    (kp_plan_host): no GPU is touched."""
+    info = KPPlanInfo()
+    _check(load().kp_plan_host(gen_pat.encode(), ctypes.c_uint32(max_block), ctypes.byref(info)))
+    return {name: getattr(info, name) for name, _ in KPPlanInfo._fields_}
 
 
 def device_count():

@@ -59,3 +59,16 @@ def test_python_baseline_runs_pyref_processes():
     r = bench.python_baseline(prep, tasks, 2)
     assert r["cores"] == 2 and r["value"] > 0 and r["single_core_value"] > 0
     assert "AAMNAA" in r["sample"]
+
+
+def test_shadow_ranks_run_host_side_without_gpu():
+    """The 2/4/8-GPU model's stand-ins for other ranks: separate processes that do a rank's
+    host side (host plan build, counts in k-mer order, fold split) on request, no GPU."""
+    sh = bench.Shadows(2, "9mer", "NNMNN")
+    try:
+        for _ in range(2):
+            sh.go(2)
+            secs = sh.wait(2)
+            assert len(secs) == 2 and all(s > 0 for s in secs)
+    finally:
+        sh.close()
