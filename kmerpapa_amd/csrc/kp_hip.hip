@@ -1005,8 +1005,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
 #endif
     KP_HIP(hipEventRecord(c->ev[0], c->stream));
     // lane classes: runs of device groups with equal lane counts (dg is sorted by width);
-    // one launch per (class, high level).  With several classes, class q > 0 runs its whole
-    // launch sequence on side stream q - 1 (KP_CLASS_STREAMS=0: everything on one stream)
+    // one launch per (class, high level).  With several classes and KP_CLASS_STREAMS=1,
+    // class q > 0 runs its whole launch sequence on side stream q - 1
     std::vector<std::pair<size_t, size_t>> classes;
     for (size_t i = 0; i < dg.size();) {
         size_t j = i;
@@ -1014,7 +1014,10 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         classes.emplace_back(i, j);
         i = j;
     }
-    const bool multi = classes.size() > 1 && !(getenv("KP_CLASS_STREAMS") && atoi(getenv("KP_CLASS_STREAMS")) == 0);
+    // KP_CLASS_STREAMS=1 runs the classes concurrently.  Off by default: measured on one
+    // MI355X, 9-mer passes of 4+3 lanes (one 7-penalty group) 620 -> 603 ms and 5+1 / 4+2
+    // (two groups) -0.5 %, but the 11-mer step (4+3 lanes, ANNNNMNNNNA) 606 -> 627 ms
+    const bool multi = classes.size() > 1 && getenv("KP_CLASS_STREAMS") && atoi(getenv("KP_CLASS_STREAMS")) == 1;
     if (multi) {
         KP_HIP(hipEventRecord(c->ev[3], c->stream));
         for (size_t q = 1; q < classes.size() && q <= KP_SIDE_STREAMS; ++q)

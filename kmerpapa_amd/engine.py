@@ -582,11 +582,10 @@ PASS_LANES = int(os.environ.get("KMERPAPA_PASS_LANES", "7"))
 
 def pass_cap(groups, fit):
     """Lanes per pass: up to PASS_LANES (7), or the largest group if wider, if that fits.
-    Groups of one pass that differ in width run as concurrent lane classes on their own
-    HIP streams (kp_hip.hip run_pass), so a small group packed beside a full one costs less
-    than alone: 9-mer passes of 4+2 lanes 531 ms against 339 + 222 sequential, 5+1 529
-    against 394 + 144; two 5-lane groups (10 lanes) never share a pass: passes of equal
-    full groups are not faster per lane and would need more HBM."""
+    A small group packed beside a full one costs less than alone (one pass's fixed work:
+    9-mer passes of 4+2 lanes 532-536 ms against 339 + 222 in two passes, 5+1 531 against
+    394 + 144); two 5-lane groups (10 lanes) never share a pass: passes of equal full groups
+    are not faster per lane and would need more HBM."""
     widest = max([len(g[3]) for g in groups] or [1])
     return min(fit, max(PASS_LANES, widest))
 
