@@ -153,7 +153,8 @@ int kp_math_log(kp_ctx *ctx, const double *x, double *y, uint64_t n);
 
 /* Parity check of the C library's log / log1p as restated for the GPU (kp_libm.h: the
  * sweep's exact fallback, the backtrack and the k-mer terms): fn 1 = log, 2 = log1p
- * (fn 0 = the device's own log, as kp_math_log), computed on the context's GPU. */
+ * (fn 0 = the device's own log, as kp_math_log; fn 3 = kp_fast_log, the sweep's table-free
+ * fdlibm log), computed on the context's GPU. */
 int kp_math_libm(kp_ctx *ctx, const double *x, double *y, uint64_t n, int fn);
 
 /* Host-only (no GPU needed): the cross-validation fold split of CV_tools.py

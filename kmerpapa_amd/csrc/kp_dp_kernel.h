@@ -76,6 +76,14 @@ struct kp_dp_params {
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
 
+// the fast path's float64 log (kp_libm.h): kp_fast_log (fdlibm, table-free) with
+// -DKP_FAST_LOG, else the device's own (ocml)
+#ifdef KP_FAST_LOG
+#define KP_DLOG(x) kp_fast_log(x)
+#else
+#define KP_DLOG(x) log(x)
+#endif
+
 // a workgroup-uniform 64-bit value (read by every lane from the same LDS word) into SGPRs
 __device__ inline uint64_t kp_rfl64(uint64_t v) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
@@ -353,8 +361,8 @@ kp_dp_kernel(kp_dp_params P) {
                 sc.logp = sc.log1mp = 0.0;
                 if (!sc.kmer) {
                     const double pr = kp_rate(sc.c, alpha, beta);
-                    sc.logp = log(pr);
-                    sc.log1mp = log(1.0 - pr);
+                    sc.logp = KP_DLOG(pr);
+                    sc.log1mp = KP_DLOG(1.0 - pr);
                 }
                 const double pj = G->pen[j];
                 kp_dp_cell_list<NL, 1>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, &pj, j);
@@ -383,8 +391,8 @@ kp_dp_kernel(kp_dp_params P) {
                 sc.logp = sc.log1mp = 0.0;
                 if (!sc.kmer && !KP_SKIP(P, 4)) {
                     const double pr = kp_rate(sc.c, alpha, beta);
-                    sc.logp = log(pr);
-                    sc.log1mp = log(1.0 - pr);
+                    sc.logp = KP_DLOG(pr);
+                    sc.log1mp = KP_DLOG(1.0 - pr);
                 }
                 if (!KP_SKIP(P, 8)) {
                     kp_dp_cell_list<NL, NL>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, pen);

@@ -158,3 +158,49 @@ __host__ __device__ __attribute__((noinline)) inline double kp_libm_log1p(double
     if (k == 0) return f - (hfsq - s * (hfsq + R));
     return k * ln2_hi - ((hfsq - (s * (hfsq + R) + (k * ln2_lo + c))) - f);
 }
+
+// kp_fast_log -- the sweep's fast float64 log (device and host, no table, no FMA): fdlibm's
+// __ieee754_log algorithm (the table-free ancestor of glibc's log; error < 1 ulp), written
+// branch-light for the GPU: both of fdlibm's final formulas are evaluated and one selected
+// exactly as fdlibm's branch would.  It stands in for ROCm's ocml log (85 instructions) on
+// the sweep's fast path, where any log within 2 ulp of the C library's is admissible: the
+// store guard (kp_core.h kp_store_unsafe) sends every float32 result that could depend on
+// the last bits to the C library's restated log.  |kp_fast_log - libm log| <= 1 ulp is
+// checked at build time (kp_libm_check) and on the GPU (test_device_fast_log_within_1ulp).
+// Arguments outside the normal positive range (0, subnormals, negatives, inf, NaN) take
+// the device's own log.
+__host__ __device__ inline double kp_fast_log(double x) {
+    const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
+    const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2, Lg3 = 0x1.2492494229359p-2,
+                 Lg4 = 0x1.c71c51d8e78afp-3, Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
+                 Lg7 = 0x1.2f112df3e5244p-3;
+    const uint64_t ix = kp_asu64(x);
+    int32_t hx = (int32_t)(ix >> 32);
+    if (__builtin_expect(hx < 0x00100000 || hx >= 0x7ff00000, 0)) return log(x);
+    int32_t k = (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int32_t i0 = (hx + 0x95f64) & 0x100000;
+    const double xn = kp_asf64(((uint64_t)(uint32_t)(hx | (i0 ^ 0x3ff00000)) << 32) | (ix & 0xffffffffull));
+    k += (i0 >> 20);
+    const double f = xn - 1.0;
+    const double dk = (double)k;
+    if (__builtin_expect((0x000fffff & (2 + hx)) < 3, 0)) {  // -2^-20 <= f < 2^-20
+        if (f == 0.0) return k == 0 ? 0.0 : dk * ln2_hi + dk * ln2_lo;
+        const double R = f * f * (0.5 - 0.33333333333333333 * f);
+        return k == 0 ? f - R : dk * ln2_hi - ((R - dk * ln2_lo) - f);
+    }
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    const double w = z * z;
+    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    const double R = t2 + t1;
+    const bool big = ((hx - 0x6147a) | (0x6b851 - hx)) > 0;
+    const double hfsq = 0.5 * f * f;
+    // fdlibm: if big  f - (hfsq - s*(hfsq+R))  /  dk*ln2_hi - ((hfsq - (s*(hfsq+R) + dk*ln2_lo)) - f)
+    //         else    f - s*(f-R)              /  dk*ln2_hi - ((s*(f-R) - dk*ln2_lo) - f)
+    const double a = big ? hfsq - s * (hfsq + R) : s * (f - R);
+    if (k == 0) return f - a;
+    const double b = big ? hfsq - (s * (hfsq + R) + dk * ln2_lo) : s * (f - R) - dk * ln2_lo;
+    return dk * ln2_hi - (b - f);
+}

@@ -31,7 +31,17 @@ static double unit() { return (double)(next_u64() >> 11) * 0x1p-53; }
 // bit-identical, NaNs included (glibc passes an input NaN through with its sign and payload)
 static bool same(double a, double b) { return memcmp(&a, &b, sizeof(double)) == 0; }
 
-static long g_bad = 0, g_n = 0;
+static long g_bad = 0, g_n = 0, g_fast_far = 0, g_fast_diff = 0;
+
+// distance in units in the last place between two finite doubles of the same sign
+static uint64_t ulps(double a, double b) {
+    int64_t ia, ib;
+    memcpy(&ia, &a, 8);
+    memcpy(&ib, &b, 8);
+    if (ia < 0) ia = INT64_MIN - ia;
+    if (ib < 0) ib = INT64_MIN - ib;
+    return ia > ib ? (uint64_t)(ia - ib) : (uint64_t)(ib - ia);
+}
 
 static void one(double x) {
     // volatile: the host compiler must call libm, not fold the call with its own arithmetic
@@ -42,6 +52,18 @@ static void one(double x) {
     if (!same(ref_log, got_log)) {
         if (g_bad < 5) fprintf(stderr, "kp_libm_check: log(%a) libm %a restated %a\n", x, ref_log, got_log);
         ++g_bad;
+    }
+    // the sweep's fast log: within 1 ulp of the C library's (the store guard's premise
+    // allows 2); only finite results of the normal positive range are its own
+    if (x > 0x1p-1022 && x < HUGE_VAL) {
+        const double fl = kp_fast_log(x), fl1 = kp_fast_log(1.0 - x);
+        const uint64_t d = ulps(fl, ref_log), d1 = (1.0 - x > 0x1p-1022) ? ulps(fl1, log((volatile double)(1.0 - x))) : 0;
+        g_fast_diff += (d != 0) + (d1 != 0);
+        if (d > 1 || d1 > 1) {
+            if (g_fast_far < 5) fprintf(stderr, "kp_libm_check: fast log(%a) off by %llu / %llu ulp\n", x,
+                                        (unsigned long long)d, (unsigned long long)d1);
+            ++g_fast_far;
+        }
     }
     if (!same(ref_log1p, got_log1p)) {
         if (g_bad < 5) fprintf(stderr, "kp_libm_check: log1p(%a) libm %a restated %a\n", -x, ref_log1p, got_log1p);
@@ -61,6 +83,11 @@ int main() {
     const double special[] = {0.0, -0.0, 1.0, 0.5, 2.0, 0x1p-1074, 0x1p-1022, 0x1.fffffffffffffp-1,
                               0x1.0000000000001p0, 1e-300, 1e300, HUGE_VAL, -1.0, -2.0, NAN, -NAN};
     for (double x : special) one(x);
+    if (g_fast_far) {
+        fprintf(stderr, "kp_libm_check: FAILED: kp_fast_log more than 1 ulp from the C library's log on %ld inputs\n",
+                g_fast_far);
+        return 1;
+    }
     if (g_bad) {
         fprintf(stderr,
                 "kp_libm_check: FAILED: %ld of %ld log/log1p results of kp_libm.h differ from this host's C "
@@ -68,6 +95,7 @@ int main() {
                 g_bad, 2 * g_n);
         return 1;
     }
-    printf("kp_libm_check: kp_libm.h log/log1p bit-identical to the host C library on %ld inputs\n", 2 * g_n);
+    printf("kp_libm_check: kp_libm.h log/log1p bit-identical to the host C library on %ld inputs; kp_fast_log "
+           "within 1 ulp of its log (%ld of the results differ)\n", 2 * g_n, g_fast_diff);
     return 0;
 }

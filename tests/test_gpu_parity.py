@@ -468,6 +468,27 @@ def test_device_log_vs_libm(eng):
     assert np.isneginf(eng.get_device(0).log(np.array([0.0]))[0])
 
 
+def test_device_fast_log_within_1ulp(eng):
+    """The table-free fdlibm log (kp_fast_log, fn 3 of kp_math_libm; the sweep's fast-path
+    log in -DKP_FAST_LOG builds) on the GPU against the box's C library: within 1 ulp on
+    the DP's range and across the whole normal range, as the store guard's premise needs
+    (<= 2 ulp; kp_core.h kp_store_unsafe)."""
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.log.argtypes = [ctypes.c_double]
+    libm.log.restype = ctypes.c_double
+    rng = np.random.RandomState(8)
+    n = 100_000
+    x = np.concatenate([rng.uniform(0.0, 1.0, n), 1.0 - rng.uniform(0.0, 0.07, n), rng.uniform(0.0, 1e-3, n),
+                        np.exp(rng.uniform(-700.0, 709.0, n)),
+                        np.array([1.0, 2.0, 0.5, 2.2250738585072014e-308, np.nextafter(1.0, 0), np.nextafter(1.0, 2)])])
+    got = eng.get_device(0).libm(x, 3)
+    want = np.array([libm.log(float(v)) for v in x])
+    ulps = np.abs(got.view(np.int64) - want.view(np.int64))
+    assert ulps.max() <= 1, x[np.argmax(ulps)]
+    assert np.isneginf(eng.get_device(0).libm(np.array([0.0]), 3)[0])
+
+
 def test_uint64_counts_multilevel_vs_oracle(eng):
     """Counts whose total exceeds 2^32 - 1 take the reference's uint64 itype (CV :94-97):
     the 64-bit count tables and kernels (their larger LDS tables put 4 lanes in a workgroup

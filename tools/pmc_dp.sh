@@ -1,6 +1,7 @@
 #!/bin/bash
 # PMC passes over one bench step (each pass its own run; <= 8 SQ / 4 TCC counters per pass).
 # usage: tools/pmc_dp.sh OUTDIR [env assignments...]; writes OUTDIR/<pass>/*counter_collection.csv
+# BENCH_ARGS: extra bench.py arguments (e.g. "--config 11mer")
 out=$1; shift
 for kv in "$@"; do export "$kv"; done
 mkdir -p "$out"
@@ -9,7 +10,7 @@ R=$GRAFT_REPO_ROOT
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$R/$out/$name" -o run -- \
-    python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-full-cv > "$R/$out/$name.log" 2>&1
+    python3 "$R/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-full-cv $BENCH_ARGS > "$R/$out/$name.log" 2>&1
   local rc=$?
   echo "pass $name rc=$rc"
   [ $rc -eq 0 ] || exit $rc  # a failed GPU step ends the script
