@@ -512,9 +512,11 @@ def main():
                 "kernel_ms_per_pass": dp_ms / a.steps, "launches_per_pass": launches / a.steps,
                 "avg_launch_ms": dp_ms / max(1, launches),
                 "bytes_per_unit": must / units_rank,
-                "basis": "achieved = bytes the blocked sweep must move per pass ((8 P_high + 4) B per unit: "
-                         "two child-row reads per high-position split pair + one score write; DESIGN.md 3) / "
-                         "HIP-event time of the pass's kp_dp_kernel launches",
+                "basis": "achieved = ALGORITHMIC (effective) bandwidth, not a measured HBM rate: the bytes the "
+                         "blocked sweep must move per pass ((8 P_high + 4) B per unit: two child-row reads per "
+                         "high-position split pair + one score write; DESIGN.md 3) / HIP-event time of the pass's "
+                         "kp_dp_kernel launches; part of those bytes are Infinity-Cache hits, so the measured "
+                         "fabric figure is traffic_frac",
                 "floor_bytes_per_unit": 8.0, "floor_frac": floor / dp_s / 1e9 / PEAK_HBM_GBS,
                 "naive_equivalent_bytes_per_unit": naive / units_rank,
                 "naive_equivalent_gbs": naive / dp_s / 1e9}
