@@ -142,15 +142,15 @@ _toolchain = None
 
 
 def toolchain_version():
-    """``hipcc --version`` text (the compiler that builds the library; part of kernel_tag)."""
+    """``hipcc --version`` of the compiler that built the library, recorded by the build
+    (csrc/kp_toolchain.txt; part of kernel_tag)."""
     global _toolchain
     if _toolchain is None:
-        import subprocess
-        hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
         try:
-            _toolchain = subprocess.run([hipcc, "--version"], capture_output=True, text=True, timeout=60).stdout
-        except (OSError, subprocess.SubprocessError):
-            _toolchain = "hipcc: unavailable"
+            with open(os.path.join(_HERE, "csrc", "kp_toolchain.txt")) as f:
+                _toolchain = f.read()
+        except OSError:
+            _toolchain = "toolchain: not recorded (library not built by csrc/Makefile)"
     return _toolchain
 
 
