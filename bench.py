@@ -239,10 +239,11 @@ def committed_traffic(gen_pat, n_lanes, kernel_tag):
 
 def cv_shares(prep, world, cap):
     """The passes each of ``world`` ranks runs for the full grid (lane-granular shares,
-    kmerpapa_amd.shard.rank_groups, packed into passes of at most ``cap`` lanes)."""
-    from kmerpapa_amd.engine import pack_passes
+    kmerpapa_amd.shard.rank_groups, in engine.plan_passes' fold order, at most ``cap`` lanes
+    per pass)."""
+    from kmerpapa_amd.engine import plan_passes
     from kmerpapa_amd.shard import rank_groups
-    return [pack_passes(rank_groups(prep["groups"], r, world), cap) for r in range(world)]
+    return [plan_passes(rank_groups(prep["groups"], r, world), cap)[0] for r in range(world)]
 
 
 def cv_run(plan, prep, gen_pat, groups):

@@ -885,7 +885,9 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     // split user groups into device groups that fit two workgroups per CU in LDS when
     // possible (LDS is the occupancy limit of the sweep)
     int per_wg = lanes_per_wg_default();
-    const size_t lds_two = std::min<size_t>(c->lds_max, 160u * 1024u / 2u);
+    // (KP_LDS_BUDGET: another per-workgroup LDS budget, e.g. one workgroup per CU; A/B only)
+    const size_t lds_two = std::min<size_t>(c->lds_max, getenv("KP_LDS_BUDGET") ? (size_t)atol(getenv("KP_LDS_BUDGET"))
+                                                                               : 160u * 1024u / 2u);
     while (per_wg > 1 && dp_lds_bytes(hp, per_wg, sizeof(CT)) > lds_two) --per_wg;
     if (dp_lds_bytes(hp, 1, sizeof(CT)) > c->lds_max) return fail(KP_E_ARG, "block does not fit LDS");
     std::vector<kp_group_dev> dg;

@@ -135,7 +135,7 @@ def _ptr(a):
 # launch knobs read by kp_hip.hip (every setting gives the same scores; they change timing)
 LAUNCH_KNOBS = ("KP_DP_THREADS", "KP_LANES_PER_WG", "KP_XCD_REMAP", "KP_LANE_SPLIT", "KP_NT_STORE", "KP_NT_SLOW",
                 "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER", "KP_EXACT_LOGS",
-               "KP_CLASS_STREAMS", "KP_NT_SLOW_H")
+               "KP_CLASS_STREAMS", "KP_NT_SLOW_H", "KP_LDS_BUDGET")
 
 
 _toolchain = None
@@ -607,6 +607,30 @@ def pack_passes(groups, max_lanes):
     return passes
 
 
+def plan_passes(groups, max_lanes):
+    """The passes one GPU runs for ``groups``, in run order: the groups are ordered by fold
+    (stable; fold -1, the fit, first) and packed into passes of at most ``max_lanes`` lanes.
+    Folds are drawn in order (CV_tools.fold_stream), so the first pass can start as soon as
+    the lowest fold of the share is drawn, and a small group is packed beside the group of
+    the nearest fold.  Returns ``(passes, order)``: ``order[i]`` = index in ``groups`` of the
+    i-th group in run order (lanes of the passes' results follow that order)."""
+    order = sorted(range(len(groups)), key=lambda i: groups[i][0])
+    return pack_passes([groups[i] for i in order], max_lanes), order
+
+
+def unpermute_lanes(groups, order, arr):
+    """Lane results of ``groups`` taken in ``order`` (plan_passes) back to the groups' own
+    group-major lane order."""
+    start = np.cumsum([0] + [len(g[3]) for g in groups])
+    out = np.empty_like(arr)
+    pos = 0
+    for i in order:
+        n = len(groups[i][3])
+        out[start[i]:start[i] + n] = arr[pos:pos + n]
+        pos += n
+    return out
+
+
 _devices = {}
 _plans = {}
 _cache_lock = threading.Lock()
@@ -688,7 +712,7 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0):
     def prep(dev, rep, chunk):
         if chunk:
             plan = get_plan(dev, gen_pat, max_block, replica=rep)
-            passes = pack_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
+            passes, _ = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
             plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
     threads = [threading.Thread(target=prep, args=(dev, rep, chunk))
                for dev, rep, chunk in zip(devices, _replicas(devices), _device_shares(groups, devices))]
@@ -730,20 +754,20 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
                     plan.counts_begin(feed.M_all, feed.U_all, feed.nf)
                 else:
                     plan.set_counts(M, U)
-                passes = pack_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
+                # passes in fold order (folds arrive in order), small groups beside a full one
+                passes, order = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
                 plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))  # one allocation
-                outs = [None] * len(passes)
-                # folds arrive in order: passes whose folds come first run first
-                order = sorted(range(len(passes)), key=lambda i: max(g[0] for g in passes[i]))
+                outs = []
                 have = set()
-                for i in order:
+                for pas in passes:
                     if feed is not None:
-                        for f in sorted({g[0] for g in passes[i] if g[0] >= 0} - have):
+                        for f in sorted({g[0] for g in pas if g[0] >= 0} - have):
                             plan.counts_fold(f, *feed.get(f))
                             have.add(f)
-                    outs[i] = plan.run(passes[i])
+                    outs.append(plan.run(pas))
             if outs:
-                results[slot] = tuple(np.concatenate([o[i] for o in outs]) for i in range(3))
+                results[slot] = tuple(unpermute_lanes(chunk, order, np.concatenate([o[i] for o in outs]))
+                                      for i in range(3))
             else:
                 results[slot] = (np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(0, np.uint64))
         except Exception as e:  # re-raised in the caller's thread

@@ -29,7 +29,10 @@ def test_cv_shares_cover_every_lane_once():
         cap = engine.pass_cap(prep["groups"], 9)
         shares = bench.cv_shares(prep, world, cap)
         got = [(g[0], g[1], c) for passes in shares for p in passes for g in p for c in g[3]]
-        assert got == want
+        assert sorted(got) == sorted(want) and len(got) == len(want)
+        for passes in shares:  # passes in fold order
+            folds = [g[0] for p in passes for g in p]
+            assert folds == sorted(folds)
         assert all(sum(len(g[3]) for g in p) <= cap for passes in shares for p in passes)
         lanes = [sum(len(g[3]) for p in passes for g in p) for passes in shares]
         assert max(lanes) - min(lanes) <= 1
@@ -44,6 +47,18 @@ def test_pass_cap_packs_small_groups_beside_full_ones():
     # an 8-rank share of the 5x5x5 grid: [5, 5, 5, 1] -> passes [5], [5], [5, 1]
     share = [(f, 1.0, 1.0, [1.0] * n) for f, n in enumerate([5, 5, 5, 1])]
     assert [[len(g[3]) for g in p] for p in engine.pack_passes(share, engine.pass_cap(share, 9))] == [[5], [5], [5, 1]]
+
+
+def test_plan_passes_fold_order_and_lane_mapping():
+    """A share [f4: 2 lanes, f0: 5, f1: 5, f2: 4] runs as passes [f0], [f1], [f2 + f4]: the
+    first pass needs only fold 0 (drawn first); results map back to the share's lane order."""
+    share = [(4, 1.0, 1.0, [1.0, 2.0]), (0, 2.0, 1.0, [1.0] * 5), (1, 2.0, 1.0, [1.0] * 5), (2, 2.0, 1.0, [1.0] * 4)]
+    passes, order = engine.plan_passes(share, engine.pass_cap(share, 9))
+    assert [[(g[0], len(g[3])) for g in p] for p in passes] == [[(0, 5)], [(1, 5)], [(2, 4), (4, 2)]]
+    lane_ids = np.arange(16)  # lane ids in the share's own order
+    run = np.concatenate([lane_ids[[0, 1]] if i == 0 else lane_ids[2:7] if i == 1 else lane_ids[7:12] if i == 2
+                          else lane_ids[12:16] for i in order])  # what the passes return, in run order
+    assert (engine.unpermute_lanes(share, order, run) == lane_ids).all()
 
 
 def test_host_cores_positive():
