@@ -608,14 +608,29 @@ def pack_passes(groups, max_lanes):
 
 
 def plan_passes(groups, max_lanes):
-    """The passes one GPU runs for ``groups``, in run order: the groups are ordered by fold
-    (stable; fold -1, the fit, first) and packed into passes of at most ``max_lanes`` lanes.
-    Folds are drawn in order (CV_tools.fold_stream), so the first pass can start as soon as
-    the lowest fold of the share is drawn, and a small group is packed beside the group of
-    the nearest fold.  Returns ``(passes, order)``: ``order[i]`` = index in ``groups`` of the
-    i-th group in run order (lanes of the passes' results follow that order)."""
-    order = sorted(range(len(groups)), key=lambda i: groups[i][0])
-    return pack_passes([groups[i] for i in order], max_lanes), order
+    """The passes one GPU runs for ``groups``, in run order: lowest fold first (folds are
+    drawn in order, CV_tools.fold_stream, so the first pass starts as soon as the share's
+    lowest fold is drawn), at most ``max_lanes`` lanes per pass.  The groups are packed in
+    descending fold order and the passes then reversed, so a small group (e.g. a 1-lane
+    piece of a split group) joins the pass of a group with the same or a HIGHER fold and
+    never delays an earlier one.  Returns ``(passes, order)``: ``order[i]`` = index in
+    ``groups`` of the i-th group in run order (the lanes of the passes' results follow it)."""
+    desc = sorted(range(len(groups)), key=lambda i: -groups[i][0])  # stable
+    passes, cur, n = [], [], 0
+    for i in desc:
+        lanes = len(groups[i][3])
+        if cur and n + lanes > max_lanes:
+            passes.append(cur)
+            cur, n = [], 0
+        cur.append(i)
+        n += lanes
+    if cur:
+        passes.append(cur)
+    if max_lanes < 1:
+        raise KPError(-2, "the lattice does not fit device memory even for one lane")
+    passes.reverse()
+    order = [i for pas in passes for i in pas]
+    return [[groups[i] for i in pas] for pas in passes], order
 
 
 def unpermute_lanes(groups, order, arr):
