@@ -237,13 +237,13 @@ def committed_traffic(gen_pat, n_lanes, kernel_tag):
     return best
 
 
-def cv_shares(prep, world, cap):
+def cv_shares(prep, world, cap, width=None):
     """The passes each of ``world`` ranks runs for the full grid (lane-granular shares,
     kmerpapa_amd.shard.rank_groups, in engine.plan_passes' fold order, at most ``cap`` lanes
-    per pass)."""
+    per pass, fold pieces of ``width`` lanes)."""
     from kmerpapa_amd.engine import plan_passes
     from kmerpapa_amd.shard import rank_groups
-    return [plan_passes(rank_groups(prep["groups"], r, world), cap)[0] for r in range(world)]
+    return [plan_passes(rank_groups(prep["groups"], r, world), cap, width)[0] for r in range(world)]
 
 
 def cv_run(plan, prep, gen_pat, groups):
@@ -460,18 +460,22 @@ def main():
     plan = engine.get_plan(prep["device"], gen_pat, a.max_block)
     prep["t_plan"] = time.perf_counter() - t0
     cap = engine.pass_cap(groups, plan.lanes_that_fit())
+    width = plan.info["lanes_per_workgroup"]
+    # a step = one pass of the whole grid's CV plan on one GPU (engine.plan_passes: fold
+    # pieces of one workgroup's lanes; 9-mer: one (alpha, fold) group of 5 penalties; 11-mer:
+    # 5 of a fold's 49 (alpha, c) lanes, some spanning two alphas)
+    step_passes = engine.plan_passes(groups, cap, width)[0]
     model_worlds = tuple(int(x) for x in a.model_worlds.split(",") if x.strip())
     worlds = () if a.no_full_cv else ((world,) + model_worlds if world == 1 else (world,))
-    most = max([len(groups[0][3])] + [sum(len(g[3]) for g in p) for w in worlds
-                                      for passes in cv_shares(prep, w, cap) for p in passes])
+    most = max([sum(len(g[3]) for g in p) for p in step_passes] +
+               [sum(len(g[3]) for g in p) for w in worlds for passes in cv_shares(prep, w, cap, width) for p in passes])
     t0 = time.perf_counter()
     plan.reserve(most)  # the one large allocation of the run (lane buffers, first-touched)
     prep["t_alloc"] = time.perf_counter() - t0
     plan.set_counts(prep["Mk"], prep["Uk"])
 
     def step(s):
-        g = groups[(s * world + rank) % len(groups)]
-        plan.run([g])
+        plan.run(step_passes[(s * world + rank) % len(step_passes)])
         return plan.stats()
 
     for s in range(a.warmup):
@@ -500,7 +504,7 @@ def main():
     must = sum(s["gather_bytes"] for s in stats)  # (8 P_high + 4) B per unit, blocked sweep
     naive = sum(s["alg_bytes"] for s in stats)     # SURVEY.md 8(d) per-cell figure
     floor = 8.0 * units_rank                       # every row read once + written once
-    lanes = len(groups[0][3])
+    lanes = round(units_rank / a.steps / plan.info["npat"])  # lanes per step (pieces of a fold may be narrower)
     tag = engine.kernel_tag()
     tr = committed_traffic(gen_pat, lanes, tag)
 
@@ -548,8 +552,8 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"synthetic {len(gen_pat)}-mer counts, general pattern {gen_pat} "
                                    f"({plan.info['npat']} cells), {len(prep['alphas'])}x{len(prep['penalties'])} "
-                                   f"(alpha, c) grid, {prep['nfolds']}-fold CV; step = one (alpha, fold) group x "
-                                   f"{lanes} penalties over the whole lattice",
+                                   f"(alpha, c) grid, {prep['nfolds']}-fold CV; step = one pass of the grid's CV plan: "
+                                   f"{lanes} (alpha, fold, c) lanes of one fold over the whole lattice",
                        "name": a.config, "gen_pat": gen_pat, "cells": plan.info["npat"], "lanes_per_step": lanes,
                        "units_per_step": plan.info["npat"] * lanes, "block_cells": plan.info["block"],
                        "alphas": prep["alphas"], "penalties": prep["penalties"], "nfolds": prep["nfolds"]},

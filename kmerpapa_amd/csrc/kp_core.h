@@ -43,16 +43,29 @@ struct kp_postab {
     uint8_t pb[16][8];
 };
 
-// one (alpha, fold) group of lanes; fold < 0 = fit mode (train counts = all data)
+// one (alpha, fold) group of lanes; fold < 0 = fit mode (train counts = all data).  A
+// mixed group (nl2 > 0) holds the lanes of two user groups of the same fold: its last nl2
+// lanes take (alpha2, beta2) -- the count tables are shared, only the logs differ
 struct kp_group_dev {
     int32_t fold;
     int32_t lane0;
     int32_t nl;
-    int32_t pad_;
+    int32_t nl2;
     double alpha;
     double beta;
     double pen[KP_GROUP_LANES];
+    double alpha2;
+    double beta2;
 };
+
+// (alpha, beta) of lane j (0-based inside the group)
+__host__ __device__ inline bool kp_lane_set2(const kp_group_dev &G, int j) { return j >= G.nl - G.nl2; }
+__host__ __device__ inline double kp_lane_alpha(const kp_group_dev &G, int j) {
+    return kp_lane_set2(G, j) ? G.alpha2 : G.alpha;
+}
+__host__ __device__ inline double kp_lane_beta(const kp_group_dev &G, int j) {
+    return kp_lane_set2(G, j) ? G.beta2 : G.beta;
+}
 
 // lattice geometry, passed by value to every kernel
 struct kp_geom {
@@ -215,6 +228,9 @@ struct kp_single_ctx {
     double logp, log1mp;
     kp_cnt c;
     bool exact;     // every cell takes the C library's logs (KP_EXACT_LOGS=1, or !kp_fast_logs_ok)
+    // mixed groups only (the MIX instantiations): lanes j >= js take the second set
+    int js;
+    double a2, b2, logp2, log1mp2;
 };
 
 // ---------------------------------------------------------------------------
@@ -292,28 +308,40 @@ __host__ __device__ inline bool kp_fast_logs_ok(const double *pen, int n, double
     return ok;
 }
 
-// a cell's final score per lane: min(best split, single term)
-template <int W, typename SP>
+// a cell's final score per lane: min(best split, single term).  MIX: lanes j0 + j >= sc.js
+// take the second (alpha, beta) set (sc.logp2 / sc.log1mp2; sc.a2 / sc.b2)
+template <int W, bool MIX = false, typename SP>
 __host__ __device__ inline void kp_cell_store(SP row, const float *lmin, const kp_single_ctx &sc, const double *pen,
-                                              double alpha, double beta) {
+                                              double alpha, double beta, uint32_t j0 = 0) {
     float out[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-        const double s = kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
+        const bool s2 = MIX && (int)(j0 + j) >= sc.js;
+        const double s = kp_single_train(sc.c, s2 ? sc.logp2 : sc.logp, s2 ? sc.log1mp2 : sc.log1mp, pen[j]);
         out[j] = s < (double)lmin[j] ? (float)s : lmin[j];  // float64 compare against the float32 store (CV :71)
     }
     bool unsafe = sc.exact;
 #pragma unroll
-    for (int j = 0; j < W; ++j)  // (every lane, stored or not: cheaper than telling them apart)
-        unsafe = unsafe || kp_store_unsafe(kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]));
+    for (int j = 0; j < W; ++j) {  // (every lane, stored or not: cheaper than telling them apart)
+        const bool s2 = MIX && (int)(j0 + j) >= sc.js;
+        unsafe = unsafe || kp_store_unsafe(kp_single_train(sc.c, s2 ? sc.logp2 : sc.logp, s2 ? sc.log1mp2 : sc.log1mp,
+                                                           pen[j]));
+    }
     if (__builtin_expect(unsafe, 0)) {  // the C library's logs (rare; laid out away from the hot path)
         const double p = kp_rate(sc.c, alpha, beta);
         const double lp = kp_libm_log(p), l1p = kp_libm_log(1.0 - p);
+        double lp2 = lp, l1p2 = l1p;
+        if (MIX && (int)(j0 + W) > sc.js) {
+            const double p2 = kp_rate(sc.c, sc.a2, sc.b2);
+            lp2 = kp_libm_log(p2);
+            l1p2 = kp_libm_log(1.0 - p2);
+        }
 #pragma unroll
         for (int j = 0; j < W; ++j) {
+            const bool s2 = MIX && (int)(j0 + j) >= sc.js;
             float best = lmin[j];
-            const double s = kp_single_train(sc.c, lp, l1p, pen[j]);
-            if (s < (double)best) best = (float)s;
+            const double v = kp_single_train(sc.c, s2 ? lp2 : lp, s2 ? l1p2 : l1p, pen[j]);
+            if (v < (double)best) best = (float)v;
             out[j] = best;
         }
     }
@@ -395,14 +423,17 @@ __host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0,
 // 4-pair chunks, the first KP_PRE_CHUNKS already loaded into pre[] by the caller (so the
 // loads overlap the logs), the rest read from lp.  The wave runs as many chunks as its
 // longest list; shorter lists end in (B, B) pairs that read the +inf slot B.
-template <int NL, int W, typename SP>
+template <int NL, int W, bool MIX = false, typename SP>
 __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, const uint4 *pre, const uint4 *lp, SP st,
                                                 const kp_single_ctx &sc, double alpha, double beta,
                                                 const double *pen, uint32_t j0 = 0) {
     SP row = st + l * NL + j0;
     if (__builtin_expect(sc.kmer, 0)) {  // level 0 (CV :145-151 / Fit :106-114)
 #pragma unroll
-        for (int j = 0; j < W; ++j) row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
+        for (int j = 0; j < W; ++j) {
+            const bool s2 = MIX && (int)(j0 + j) >= sc.js;
+            row[j] = kp_kmer_train(sc.c, s2 ? sc.a2 : alpha, s2 ? sc.b2 : beta, pen[j]);
+        }
         return;
     }
     float lmin[W];
@@ -425,7 +456,7 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
         if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
     for (uint32_t k = KP_PRE_CHUNKS; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
 #endif
-    kp_cell_store<W>(row, lmin, sc, pen, alpha, beta);
+    kp_cell_store<W, MIX>(row, lmin, sc, pen, alpha, beta, j0);
 }
 
 // ---------------------------------------------------------------------------

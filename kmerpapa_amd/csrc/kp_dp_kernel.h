@@ -193,8 +193,10 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
 #endif
 // HZ: the build that handles k-mer cells (only high level 0's blocks hold them; their
 // xlogy / xlog1py terms call the C library's logs, kp_libm.h); launches of higher levels
-// may use the build without that code (kp_hip.hip launch_dp)
-template <typename CT, int NL, bool HZ>
+// may use the build without that code (kp_hip.hip launch_dp).  MIX: the build for launch
+// classes that hold mixed groups (kp_group_dev.nl2 > 0: a second (alpha, beta) set for the
+// group's last lanes, a second pair of logs per cell); other classes use MIX = false
+template <typename CT, int NL, bool HZ, bool MIX>
 __global__ void __launch_bounds__(KP_DP_MAX_THREADS) __attribute__((amdgpu_waves_per_eu(NL <= 3 ? KP_SMALL_WAVES : 1)))
 kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -223,7 +225,11 @@ kp_dp_kernel(kp_dp_params P) {
     double pen[NL];
 #pragma unroll
     for (int j = 0; j < NL; ++j) pen[j] = G->pen[j];
-    const bool exact = P.exact != 0 || !kp_fast_logs_ok(G->pen, G->nl, alpha, beta);
+    // mixed group: lanes js.. take (alpha2, beta2); js = NL when the group is not mixed
+    const int js = MIX ? G->nl - G->nl2 : NL;
+    const double alpha2 = MIX ? G->alpha2 : alpha, beta2 = MIX ? G->beta2 : beta;
+    const bool exact = P.exact != 0 || !kp_fast_logs_ok(G->pen, G->nl, alpha, beta) ||
+                       (MIX && js < NL && !kp_fast_logs_ok(G->pen, G->nl, alpha2, beta2));
 
     // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | lm[t][16]
     //      (count-table scratch aliases st, which the gather fills afterwards; every carve
@@ -359,13 +365,15 @@ kp_dp_kernel(kp_dp_params P) {
                 sc.kmer = high_zero && lam == 0;
                 sc.c.mte = sc.c.ute = 0;
                 sc.logp = sc.log1mp = 0.0;
+                // one lane per thread: its own (alpha, beta) set
+                const double aj = (MIX && (int)j >= js) ? alpha2 : alpha, bj = (MIX && (int)j >= js) ? beta2 : beta;
                 if (!sc.kmer) {
-                    const double pr = kp_rate(sc.c, alpha, beta);
+                    const double pr = kp_rate(sc.c, aj, bj);
                     sc.logp = KP_DLOG(pr);
                     sc.log1mp = KP_DLOG(1.0 - pr);
                 }
                 const double pj = G->pen[j];
-                kp_dp_cell_list<NL, 1>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, &pj, j);
+                kp_dp_cell_list<NL, 1>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, aj, bj, &pj, j);
             }
         } else
 #pragma unroll
@@ -394,8 +402,20 @@ kp_dp_kernel(kp_dp_params P) {
                     sc.logp = KP_DLOG(pr);
                     sc.log1mp = KP_DLOG(1.0 - pr);
                 }
+                if (MIX) {  // the second set's logs (group-uniform branch)
+                    sc.js = js;
+                    sc.a2 = alpha2;
+                    sc.b2 = beta2;
+                    sc.logp2 = sc.logp;
+                    sc.log1mp2 = sc.log1mp;
+                    if (js < NL && !sc.kmer) {
+                        const double pr2 = kp_rate(sc.c, alpha2, beta2);
+                        sc.logp2 = KP_DLOG(pr2);
+                        sc.log1mp2 = KP_DLOG(1.0 - pr2);
+                    }
+                }
                 if (!KP_SKIP(P, 8)) {
-                    kp_dp_cell_list<NL, NL>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, pen);
+                    kp_dp_cell_list<NL, NL, MIX>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, pen);
                 } else {  // timing ablation: no split scan, keep the single term
 #pragma unroll
                     for (int j = 0; j < NL; ++j)

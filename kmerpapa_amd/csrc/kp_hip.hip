@@ -164,8 +164,9 @@ __global__ void __launch_bounds__(256) kp_bt_level(kp_bt_params P) {
     const uint32_t lo = P.depth ? de[P.depth - 1] : 0u, hi = de[P.depth];
     const kp_group_dev *G = P.groups + P.lanegrp[lane];
     const int fold = G->fold;
-    const double alpha = G->alpha, beta = G->beta;
-    const double pen = G->pen[lane - (uint32_t)G->lane0];
+    const int jl = (int)(lane - (uint32_t)G->lane0);
+    const double alpha = kp_lane_alpha(*G, jl), beta = kp_lane_beta(*G, jl);
+    const double pen = G->pen[jl];
     const CT *K = reinterpret_cast<const CT *>(P.K);
     kp_node *N = P.nodes + (uint64_t)lane * P.cap;
     const uint32_t nw = (gridDim.x * blockDim.x) >> 6;
@@ -356,7 +357,9 @@ __global__ void kp_codes_kernel(kp_geom g, kp_dev_tables T, const CT *K, const f
         const uint64_t dig = kp_cell_digits(g, x);
         auto score = [&](uint64_t y) { return S[kp_s_off(g, y / g.B, lane, (uint32_t)(y % g.B))]; };
         float v;
-        code[x] = (uint8_t)kp_cell_decide(g, T.tabs, x, dig, score, c, G.alpha, G.beta, pen, &v);
+        const int jl = (int)(lane - (uint32_t)G.lane0);
+        code[x] = (uint8_t)kp_cell_decide(g, T.tabs, x, dig, score, c, kp_lane_alpha(G, jl), kp_lane_beta(G, jl), pen,
+                                          &v);
     }
 }
 
@@ -571,6 +574,8 @@ void kp_plan_destroy(kp_plan *p) {
     delete p;
 }
 
+static int wg_lanes(const kp::host_plan &hp, size_t ct_bytes, size_t lds_max);  // defined with the launch code
+
 static void info_of(const kp::host_plan &h, kp_plan_info *o) {
     o->npat = h.npat;
     o->nblocks = h.g.nblocks;
@@ -586,6 +591,8 @@ static void info_of(const kp::host_plan &h, kp_plan_info *o) {
     // train scores + backtrack node pool + leaf list
     o->bytes_per_lane = h.g.nblocks * (uint64_t)h.g.Bpad * 4 + (uint64_t)node_cap_of(h) * sizeof(kp_node) +
                         h.n_kmers * 8 + 4096;
+    o->lanes_per_workgroup = (uint32_t)wg_lanes(h, 4, 160u * 1024u);
+    o->pad_ = 0;
 }
 
 int kp_plan_get_info(const kp_plan *p, kp_plan_info *o) {
@@ -732,12 +739,12 @@ static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
         ;
 }
 
-template <typename CT, int NL, bool HZ>
+template <typename CT, int NL, bool HZ, bool MIX>
 static int launch_dp_hz(hipStream_t st, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
     if (lds > 65536)
-        KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_kernel<CT, NL, HZ>),
+        KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_kernel<CT, NL, HZ, MIX>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((kp_dp_kernel<CT, NL, HZ>), dim3(nb, ngroups), dim3(threads), lds, st, P);
+    hipLaunchKernelGGL((kp_dp_kernel<CT, NL, HZ, MIX>), dim3(nb, ngroups), dim3(threads), lds, st, P);
     KP_HIP(hipGetLastError());
     return KP_OK;
 }
@@ -745,24 +752,35 @@ static int launch_dp_hz(hipStream_t st, const kp_dp_params &P, unsigned nb, unsi
 // Groups of 1-3 lanes (80 VGPRs at 6 waves per SIMD) run high levels >= 1 without the
 // k-mer code (fewer spills: 1-lane pass 149 -> 144 ms); wider groups keep one kernel for
 // every level (the split build measured slower there: 5 lanes 395 -> 402 ms)
-template <typename CT, int NL>
+// (the mixed builds always split: their k-mer code adds register spills at every width)
+template <typename CT, int NL, bool MIX>
 static int launch_dp(hipStream_t st, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
-    return (P.H == 0 || NL > 3) ? launch_dp_hz<CT, NL, true>(st, P, nb, ngroups, threads, lds)
-                                : launch_dp_hz<CT, NL, false>(st, P, nb, ngroups, threads, lds);
+    return (P.H == 0 || (NL > 3 && !MIX)) ? launch_dp_hz<CT, NL, true, MIX>(st, P, nb, ngroups, threads, lds)
+                                : launch_dp_hz<CT, NL, false, MIX>(st, P, nb, ngroups, threads, lds);
+}
+
+// mixed groups (two (alpha, beta) sets) need at least 2 lanes
+template <typename CT, int NL>
+static int launch_dp_mix(bool mix, hipStream_t st, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads,
+                         size_t lds) {
+    if constexpr (NL >= 2) {
+        if (mix) return launch_dp<CT, NL, true>(st, P, nb, ngroups, threads, lds);
+    }
+    return launch_dp<CT, NL, false>(st, P, nb, ngroups, threads, lds);
 }
 
 template <typename CT>
-static int launch_dp_nl(int nl, hipStream_t c, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads,
-                        size_t lds) {
+static int launch_dp_nl(int nl, bool mix, hipStream_t c, const kp_dp_params &P, unsigned nb, unsigned ngroups,
+                        int threads, size_t lds) {
     switch (nl) {
-        case 1: return launch_dp<CT, 1>(c, P, nb, ngroups, threads, lds);
-        case 2: return launch_dp<CT, 2>(c, P, nb, ngroups, threads, lds);
-        case 3: return launch_dp<CT, 3>(c, P, nb, ngroups, threads, lds);
-        case 4: return launch_dp<CT, 4>(c, P, nb, ngroups, threads, lds);
-        case 5: return launch_dp<CT, 5>(c, P, nb, ngroups, threads, lds);
-        case 6: return launch_dp<CT, 6>(c, P, nb, ngroups, threads, lds);
-        case 7: return launch_dp<CT, 7>(c, P, nb, ngroups, threads, lds);
-        case 8: return launch_dp<CT, 8>(c, P, nb, ngroups, threads, lds);
+        case 1: return launch_dp_mix<CT, 1>(mix, c, P, nb, ngroups, threads, lds);
+        case 2: return launch_dp_mix<CT, 2>(mix, c, P, nb, ngroups, threads, lds);
+        case 3: return launch_dp_mix<CT, 3>(mix, c, P, nb, ngroups, threads, lds);
+        case 4: return launch_dp_mix<CT, 4>(mix, c, P, nb, ngroups, threads, lds);
+        case 5: return launch_dp_mix<CT, 5>(mix, c, P, nb, ngroups, threads, lds);
+        case 6: return launch_dp_mix<CT, 6>(mix, c, P, nb, ngroups, threads, lds);
+        case 7: return launch_dp_mix<CT, 7>(mix, c, P, nb, ngroups, threads, lds);
+        case 8: return launch_dp_mix<CT, 8>(mix, c, P, nb, ngroups, threads, lds);
     }
     return fail(KP_E_ARG, "lanes per workgroup must be 1..8");
 }
@@ -773,10 +791,27 @@ static int dp_threads() {
     return (v == 64 || v == 128 || v == 256 || v == 512 || v == 1024) ? v : 512;
 }
 
+// a wide group's lanes as full workgroups first (7 lanes as 5 + 2: 9-mer pass 603 -> 593
+// ms, profiles/r03/experiments/wide_split.txt); KP_WIDE_SPLIT=0: near-equal (4 + 3)
+static bool wide_split_greedy() {
+    const char *e = getenv("KP_WIDE_SPLIT");
+    return !e || atoi(e) != 0;
+}
+
 static int lanes_per_wg_default() {
     const char *e = getenv("KP_LANES_PER_WG");
     int v = e ? atoi(e) : 5;
     return std::min(std::max(v, 1), KP_GROUP_LANES);
+}
+
+// lanes per workgroup of the sweep: KP_LANES_PER_WG (default 5), fewer if two workgroups
+// per CU would not fit LDS (KP_LDS_BUDGET: another per-workgroup budget; A/B only)
+static int wg_lanes(const kp::host_plan &hp, size_t ct_bytes, size_t lds_max) {
+    int per_wg = lanes_per_wg_default();
+    const size_t lds_two = std::min<size_t>(lds_max, getenv("KP_LDS_BUDGET") ? (size_t)atol(getenv("KP_LDS_BUDGET"))
+                                                                            : 160u * 1024u / 2u);
+    while (per_wg > 1 && dp_lds_bytes(hp, per_wg, ct_bytes) > lds_two) --per_wg;
+    return per_wg;
 }
 
 // Score rows + backtrack node pool for `lanes` lanes.  Grown only (a pass with fewer lanes
@@ -884,37 +919,95 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     g.nf = p->nf;
     // split user groups into device groups that fit two workgroups per CU in LDS when
     // possible (LDS is the occupancy limit of the sweep)
-    int per_wg = lanes_per_wg_default();
-    // (KP_LDS_BUDGET: another per-workgroup LDS budget, e.g. one workgroup per CU; A/B only)
-    const size_t lds_two = std::min<size_t>(c->lds_max, getenv("KP_LDS_BUDGET") ? (size_t)atol(getenv("KP_LDS_BUDGET"))
-                                                                               : 160u * 1024u / 2u);
-    while (per_wg > 1 && dp_lds_bytes(hp, per_wg, sizeof(CT)) > lds_two) --per_wg;
+    const int per_wg = wg_lanes(hp, sizeof(CT), c->lds_max);
     if (dp_lds_bytes(hp, 1, sizeof(CT)) > c->lds_max) return fail(KP_E_ARG, "block does not fit LDS");
-    std::vector<kp_group_dev> dg;
-    uint32_t lane = 0;
     for (int i = 0; i < n_groups; ++i) {
         const kp_group &u = groups[i];
         if (u.n_lanes < 1 || u.n_lanes > KP_GROUP_MAX_LANES) return fail(KP_E_ARG, "group lanes must be 1..8");
         if (u.fold >= p->nf || u.fold < -1) return fail(KP_E_ARG, "fold out of range");
         if (u.fold >= 0 && !p->fold_set[u.fold])
             return fail(KP_E_STATE, "counts of fold " + std::to_string(u.fold) + " are not set (kp_counts_fold)");
-        // as few device groups as the workgroup width allows, of near-equal lane counts
-        // (a device group's cost is ~100 ms + ~60 ms per lane at 9-mers, DESIGN.md 5: 7
-        // lanes as 4 + 3 beat 5 + 2)
-        const int nd = (u.n_lanes + per_wg - 1) / per_wg;
-        for (int q = 0, s = 0; q < nd; ++q) {
-            kp_group_dev d;
-            memset(&d, 0, sizeof(d));
-            d.fold = u.fold;
-            d.lane0 = (int32_t)lane;
-            d.nl = u.n_lanes / nd + (q < u.n_lanes % nd ? 1 : 0);
-            d.alpha = u.alpha;
-            d.beta = u.beta;
-            for (int j = 0; j < d.nl; ++j) d.pen[j] = u.penalty[s + j];
-            s += d.nl;
-            lane += (uint32_t)d.nl;
-            dg.push_back(d);
+    }
+    std::vector<kp_group_dev> dg;
+    uint32_t lane = 0;
+    // lanes [s, s + n) of the run of user groups g0.. (group-major) as one device group;
+    // lanes of a second user group with another (alpha, beta) become the mixed set 2
+    auto chunk = [&](int g0, int s, int n) -> bool {
+        kp_group_dev d;
+        memset(&d, 0, sizeof(d));
+        d.fold = groups[g0].fold;
+        d.lane0 = (int32_t)lane;
+        d.nl = n;
+        d.alpha = d.alpha2 = groups[g0].alpha;
+        d.beta = d.beta2 = groups[g0].beta;
+        int gi = g0, off = s;
+        while (off >= groups[gi].n_lanes) off -= groups[gi++].n_lanes;
+        const int first = gi;
+        for (int j = 0; j < n; ++j, ++off) {
+            if (off == groups[gi].n_lanes) {
+                off = 0;
+                ++gi;
+            }
+            const kp_group &u = groups[gi];
+            if (j == 0) {
+                d.alpha = d.alpha2 = u.alpha;
+                d.beta = d.beta2 = u.beta;
+            } else if (gi != first) {
+                if (gi > first + 1) return false;  // at most two user groups per device group
+                const bool same = u.alpha == groups[first].alpha && u.beta == groups[first].beta;
+                if (!same && d.nl2 == 0) {
+                    d.alpha2 = u.alpha;
+                    d.beta2 = u.beta;
+                }
+                if (!same) ++d.nl2;
+            }
+            d.pen[j] = u.penalty[off];
         }
+        dg.push_back(d);
+        lane += (uint32_t)n;
+        return true;
+    };
+    // Each user group becomes as few device groups as the workgroup width allows, full
+    // workgroups first (wide_split_greedy).  Consecutive user groups of the same fold share their count tables: when
+    // cutting the run's lanes together gives fewer device groups, they are cut together
+    // (mixed groups, e.g. the 2 + 3 lanes of two alphas as one 5-lane group; at most two
+    // (alpha, beta) sets each; KP_MIX_GROUPS=0 disables)
+    const bool mixing = !getenv("KP_MIX_GROUPS") || atoi(getenv("KP_MIX_GROUPS")) != 0;
+    for (int i = 0; i < n_groups;) {
+        int e = i + 1, tot = groups[i].n_lanes, sep = (groups[i].n_lanes + per_wg - 1) / per_wg;
+        while (mixing && e < n_groups && groups[e].fold == groups[i].fold) {
+            tot += groups[e].n_lanes;
+            sep += (groups[e].n_lanes + per_wg - 1) / per_wg;
+            ++e;
+        }
+        const int nd = (tot + per_wg - 1) / per_wg;
+        bool merged = false;
+        if (e > i + 1 && nd < sep) {
+            const size_t dg0 = dg.size();
+            const uint32_t lane0 = lane;
+            merged = true;
+            for (int q = 0, s = 0; q < nd && merged; ++q) {
+                const int n = wide_split_greedy() ? std::min(per_wg, tot - s) : tot / nd + (q < tot % nd ? 1 : 0);
+                merged = chunk(i, s, n);
+                s += n;
+            }
+            if (!merged) {  // a chunk would span three user groups: cut them one by one
+                dg.resize(dg0);
+                lane = lane0;
+            }
+        }
+        if (!merged)
+            for (int q = i; q < e; ++q) {
+                const kp_group &u = groups[q];
+                const int nq = (u.n_lanes + per_wg - 1) / per_wg;
+                for (int r = 0, s = 0; r < nq; ++r) {
+                    const int n = wide_split_greedy() ? std::min(per_wg, u.n_lanes - s)
+                                                      : u.n_lanes / nq + (r < u.n_lanes % nq ? 1 : 0);
+                    chunk(q, s, n);
+                    s += n;
+                }
+            }
+        i = e;
     }
     const uint32_t Ltot = lane;
     g.Ltot = Ltot;
@@ -1052,7 +1145,9 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
                 }
                 KP_HIP(hipEventRecord(p->lev[2 * launches], st));
             }
-            int rc = launch_dp_nl<CT>(dg[i].nl, st, Q, (unsigned)nb, (unsigned)(j - i), threads, lds);
+            bool mix = false;
+            for (size_t q2 = i; q2 < j; ++q2) mix = mix || dg[q2].nl2 > 0;
+            int rc = launch_dp_nl<CT>(dg[i].nl, mix, st, Q, (unsigned)nb, (unsigned)(j - i), threads, lds);
             if (rc) return rc;
             if (timed) KP_HIP(hipEventRecord(p->lev[2 * launches + 1], st));
             ++launches;

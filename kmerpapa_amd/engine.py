@@ -49,7 +49,8 @@ class KPPlanInfo(ctypes.Structure):
                 ("block", ctypes.c_uint32), ("block_pad", ctypes.c_uint32), ("k", ctypes.c_int32),
                 ("low_positions", ctypes.c_int32), ("max_level", ctypes.c_int32),
                 ("high_levels", ctypes.c_int32), ("pairs_total", ctypes.c_double),
-                ("pairs_high", ctypes.c_double), ("bytes_per_lane", ctypes.c_uint64)]
+                ("pairs_high", ctypes.c_double), ("bytes_per_lane", ctypes.c_uint64),
+                ("lanes_per_workgroup", ctypes.c_uint32), ("pad_", ctypes.c_uint32)]
 
 
 class KPPassStats(ctypes.Structure):
@@ -135,7 +136,7 @@ def _ptr(a):
 # launch knobs read by kp_hip.hip (every setting gives the same scores; they change timing)
 LAUNCH_KNOBS = ("KP_DP_THREADS", "KP_LANES_PER_WG", "KP_XCD_REMAP", "KP_LANE_SPLIT", "KP_NT_STORE", "KP_NT_SLOW",
                 "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER", "KP_EXACT_LOGS",
-               "KP_CLASS_STREAMS", "KP_NT_SLOW_H", "KP_LDS_BUDGET")
+               "KP_CLASS_STREAMS", "KP_NT_SLOW_H", "KP_LDS_BUDGET", "KP_WIDE_SPLIT")
 
 
 _toolchain = None
@@ -607,42 +608,81 @@ def pack_passes(groups, max_lanes):
     return passes
 
 
-def plan_passes(groups, max_lanes):
+def fold_pieces(groups, width):
+    """The lanes of ``groups`` cut into pieces of at most ``width`` lanes, fold by fold: each
+    fold's lanes (its groups in order, group-major) are cut together, so one piece may hold
+    the last penalties of one alpha and the first of the next.  The library runs such a
+    piece as ONE device group (a mixed group: the fold's count tables are shared, only the
+    logs differ per alpha), so a 7-penalty grid runs as 5-lane workgroups instead of 5 + 2
+    per alpha.  Returns pieces in order of first appearance of their fold; a piece is a list
+    of ``(fold, alpha, beta, penalties, lane_ids)``, lane ids = group-major lane numbers in
+    ``groups``."""
+    start = np.cumsum([0] + [len(g[3]) for g in groups])
+    folds = {}
+    for gi, g in enumerate(groups):
+        folds.setdefault(g[0], []).extend((gi, j) for j in range(len(g[3])))
+    pieces = []
+    for lanes in folds.values():
+        for q in range(0, len(lanes), width):
+            piece = []
+            for gi, j in lanes[q:q + width]:
+                f, a, b, pens = groups[gi][:4]
+                if piece and piece[-1][5] == gi:
+                    piece[-1][3].append(pens[j])
+                    piece[-1][4].append(int(start[gi] + j))
+                else:
+                    piece.append([f, a, b, [pens[j]], [int(start[gi] + j)], gi])
+            pieces.append([tuple(x[:5]) for x in piece])
+    return pieces
+
+
+def plan_passes(groups, max_lanes, width=None):
     """The passes one GPU runs for ``groups``, in run order: lowest fold first (folds are
     drawn in order, CV_tools.fold_stream, so the first pass starts as soon as the share's
-    lowest fold is drawn), at most ``max_lanes`` lanes per pass.  The groups are packed in
-    descending fold order and the passes then reversed, so a small group (e.g. a 1-lane
-    piece of a split group) joins the pass of a group with the same or a HIGHER fold and
-    never delays an earlier one.  Returns ``(passes, order)``: ``order[i]`` = index in
-    ``groups`` of the i-th group in run order (the lanes of the passes' results follow it)."""
-    desc = sorted(range(len(groups)), key=lambda i: -groups[i][0])  # stable
+    lowest fold is drawn), at most ``max_lanes`` lanes per pass.  With ``width`` (the lanes
+    of one sweep workgroup, ``Plan.info["lanes_per_workgroup"]``) the lanes are first cut
+    into fold pieces of that width (fold_pieces); without it every group is one piece.
+    Pieces are packed in descending fold order and the passes then reversed, so a small
+    piece (e.g. a 1-lane piece of a split group) joins the pass of a piece with the same or
+    a HIGHER fold and never delays an earlier one.  Returns ``(passes, lane_order)``: a
+    pass is a list of groups ``(fold, alpha, beta, penalties)``; ``lane_order[k]`` = the
+    group-major lane number in ``groups`` of the k-th lane of the passes' concatenated
+    results (unpermute_lanes)."""
+    if max_lanes < 1:
+        raise KPError(-2, "the lattice does not fit device memory even for one lane")
+    if width:
+        pieces = fold_pieces(groups, max(1, min(width, max_lanes)))
+    else:
+        start = np.cumsum([0] + [len(g[3]) for g in groups])
+        pieces = [[(g[0], g[1], g[2], list(g[3]), list(range(start[i], start[i + 1])))] for i, g in enumerate(groups)]
+    desc = sorted(range(len(pieces)), key=lambda i: -pieces[i][0][0])  # stable
     passes, cur, n = [], [], 0
     for i in desc:
-        lanes = len(groups[i][3])
+        lanes = sum(len(x[3]) for x in pieces[i])
         if cur and n + lanes > max_lanes:
             passes.append(cur)
             cur, n = [], 0
-        cur.append(i)
+        cur.extend(pieces[i])
         n += lanes
     if cur:
         passes.append(cur)
-    if max_lanes < 1:
-        raise KPError(-2, "the lattice does not fit device memory even for one lane")
     passes.reverse()
-    order = [i for pas in passes for i in pas]
-    return [[groups[i] for i in pas] for pas in passes], order
+    # the first pass starts when its highest fold is drawn: if it packs the share's lowest
+    # fold with a higher one (e.g. a 1-lane fold-0 piece beside a 4-lane fold-2 piece), the
+    # lowest fold's pieces run first on their own (fold 2 is drawn ~65 ms after fold 0 at
+    # 9-mers, while packing saves ~10 ms of pass time)
+    if passes and len({x[0] for x in passes[0]}) > 1:
+        lo = min(x[0] for x in passes[0])
+        passes[:1] = [[x for x in passes[0] if x[0] == lo], [x for x in passes[0] if x[0] != lo]]
+    lane_order = np.array([lid for pas in passes for x in pas for lid in x[4]], dtype=np.int64)
+    return [[tuple(x[:4]) for x in pas] for pas in passes], lane_order
 
 
-def unpermute_lanes(groups, order, arr):
-    """Lane results of ``groups`` taken in ``order`` (plan_passes) back to the groups' own
-    group-major lane order."""
-    start = np.cumsum([0] + [len(g[3]) for g in groups])
+def unpermute_lanes(lane_order, arr):
+    """Lane results in the passes' order (plan_passes) back to the groups' own group-major
+    lane order."""
     out = np.empty_like(arr)
-    pos = 0
-    for i in order:
-        n = len(groups[i][3])
-        out[start[i]:start[i] + n] = arr[pos:pos + n]
-        pos += n
+    out[lane_order] = arr
     return out
 
 
@@ -727,7 +767,7 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0):
     def prep(dev, rep, chunk):
         if chunk:
             plan = get_plan(dev, gen_pat, max_block, replica=rep)
-            passes, _ = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
+            passes, _ = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()), plan.info["lanes_per_workgroup"])
             plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
     threads = [threading.Thread(target=prep, args=(dev, rep, chunk))
                for dev, rep, chunk in zip(devices, _replicas(devices), _device_shares(groups, devices))]
@@ -770,7 +810,8 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
                 else:
                     plan.set_counts(M, U)
                 # passes in fold order (folds arrive in order), small groups beside a full one
-                passes, order = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()))
+                passes, order = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()),
+                                            plan.info["lanes_per_workgroup"])
                 plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))  # one allocation
                 outs = []
                 have = set()
@@ -781,7 +822,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
                             have.add(f)
                     outs.append(plan.run(pas))
             if outs:
-                results[slot] = tuple(unpermute_lanes(chunk, order, np.concatenate([o[i] for o in outs]))
+                results[slot] = tuple(unpermute_lanes(order, np.concatenate([o[i] for o in outs]))
                                       for i in range(3))
             else:
                 results[slot] = (np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(0, np.uint64))

@@ -9,8 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 _PATH = os.path.join(HERE, "libkp_emu.so")
 _lib = None
 
-GROUP_DT = np.dtype([("fold", "<i4"), ("lane0", "<i4"), ("nl", "<i4"), ("pad", "<i4"),
-                     ("alpha", "<f8"), ("beta", "<f8"), ("pen", "<f8", (8,))])
+GROUP_DT = np.dtype([("fold", "<i4"), ("lane0", "<i4"), ("nl", "<i4"), ("nl2", "<i4"),
+                     ("alpha", "<f8"), ("beta", "<f8"), ("pen", "<f8", (8,)), ("alpha2", "<f8"), ("beta2", "<f8")])
 
 
 def lib():

@@ -55,12 +55,41 @@ def test_plan_passes_fold_order_and_lane_mapping():
     pass needs only fold 0 (drawn first), a small piece never delays a lower fold's pass,
     and results map back to the share's lane order."""
     share = [(4, 1.0, 1.0, [1.0, 2.0]), (0, 2.0, 1.0, [1.0] * 5), (1, 2.0, 1.0, [1.0] * 5), (2, 2.0, 1.0, [1.0] * 4)]
-    passes, order = engine.plan_passes(share, engine.pass_cap(share, 9))
-    assert [[(g[0], len(g[3])) for g in p] for p in passes] == [[(0, 5)], [(1, 5)], [(4, 2), (2, 4)]]
-    start = np.cumsum([0] + [len(g[3]) for g in share])
-    lane_ids = np.arange(16)  # lane ids in the share's own order
-    run = np.concatenate([lane_ids[start[i]:start[i + 1]] for i in order])  # what the passes return
-    assert (engine.unpermute_lanes(share, order, run) == lane_ids).all()
+    for width in (None, 5):  # 5-lane fold pieces leave this share's groups whole
+        passes, order = engine.plan_passes(share, engine.pass_cap(share, 9), width)
+        assert [[(g[0], len(g[3])) for g in p] for p in passes] == [[(0, 5)], [(1, 5)], [(4, 2), (2, 4)]]
+        lane_ids = np.arange(16)  # lane ids in the share's own order
+        run = lane_ids[order]  # what the passes return
+        assert (engine.unpermute_lanes(order, run) == lane_ids).all()
     share2 = [(2, 1.0, 1.0, [1.0]), (3, 1.0, 1.0, [1.0] * 5), (4, 1.0, 1.0, [1.0] * 5), (0, 1.0, 1.0, [1.0] * 5)]
     passes2, _ = engine.plan_passes(share2, engine.pass_cap(share2, 9))
     assert [[(g[0], len(g[3])) for g in p] for p in passes2] == [[(0, 5)], [(3, 5), (2, 1)], [(4, 5)]]
+    # a share whose lowest fold is a 1-lane piece: that piece runs alone first rather than
+    # wait (packed beside the 4-lane fold-2 piece) for fold 2 to be drawn
+    share3 = [(2, 1.0, 1.0, [1.0] * 4), (3, 1.0, 1.0, [1.0] * 5), (4, 1.0, 1.0, [1.0] * 5), (0, 2.0, 1.0, [1.0])]
+    passes3, order3 = engine.plan_passes(share3, engine.pass_cap(share3, 9), 5)
+    assert [[(g[0], len(g[3])) for g in p] for p in passes3] == [[(0, 1)], [(2, 4)], [(3, 5)], [(4, 5)]]
+    assert sorted(order3.tolist()) == list(range(15)) and order3[0] == 14
+
+
+def test_fold_pieces_cut_wide_grids_into_workgroup_widths():
+    """The 11-mer grid (7 alphas x 7 penalties x 10 folds): each fold's 49 lanes become nine
+    5-lane pieces and one 4-lane piece, a piece holding at most two alphas of one fold (the
+    library runs it as one mixed device group), every lane exactly once and in order."""
+    alphas, pens = [0.5, 1.0, 2.0, 3.0, 5.0, 7.0, 10.0], [2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0]
+    groups = [(f, a, 0.01 * a * (f + 1), list(pens)) for a in alphas for f in range(10)]
+    passes, order = engine.plan_passes(groups, engine.pass_cap(groups, 9), 5)
+    assert len(passes) == 100
+    assert sorted(order.tolist()) == list(range(490))
+    for p in passes:
+        assert len({g[0] for g in p}) == 1 and 1 <= len(p) <= 2
+        assert sum(len(g[3]) for g in p) in (4, 5)
+    folds = [p[0][0] for p in passes]
+    assert folds == sorted(folds)
+    # every lane of the passes is the (fold, alpha, penalty) its lane id names
+    lanes = [(g[0], g[1], c) for g in groups for c in g[3]]
+    got = [(g[0], g[1], c) for p in passes for g in p for c in g[3]]
+    assert got == [lanes[i] for i in order]
+    # the 5x5x5 grid: pieces are the (alpha, fold) groups themselves
+    p9, o9 = engine.plan_passes(_prep()["groups"], 7, 5)
+    assert all(len(p) == 1 and len(p[0][3]) == 5 for p in p9) and len(p9) == 25

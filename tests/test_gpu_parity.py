@@ -373,7 +373,8 @@ def test_degenerate_lattices_fit_vs_oracle(eng, gp):
 def test_lanes_per_workgroup_vs_oracle(eng, per_wg, monkeypatch):
     """Every lanes-per-workgroup kernel instantiation (KP_LANES_PER_WG; the default is 5)
     on an 8-penalty group (6 or 7 for those widths) of a small-block 5-mer, split into
-    near-equal device groups (8 lanes at width 3: 3 + 3 + 2): all cells equal the oracle's."""
+    device groups of full workgroups first (8 lanes at width 3: 3 + 3 + 2): all cells equal
+    the oracle's."""
     from kmerpapa_amd.CV_tools import fold_tables
     from kmerpapa_amd.pattern_utils import generality
     from oracle import oracle as O
@@ -390,7 +391,7 @@ def test_lanes_per_workgroup_vs_oracle(eng, per_wg, monkeypatch):
     utr = tot_u.sum() - tot_u
     betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
     pens = [0.5, 1.5, 2.5, 3.5, 4.5, 6.0, 8.0, 11.0]
-    if per_wg in (6, 7):  # groups split into near-equal device groups: 8 lanes would run as 4 + 4
+    if per_wg in (6, 7):  # one group per workgroup at these widths
         pens = pens[:per_wg]
     plan = eng.Plan(eng.get_device(0), gp, 64)
     plan.set_counts(Mk, Uk)
@@ -402,6 +403,61 @@ def test_lanes_per_workgroup_vs_oracle(eng, per_wg, monkeypatch):
             score, _ = plan.dump_lane(lane)
             assert bits_equal(score, ref["score"][:, f]), (gp, per_wg, c, f)
             assert bits_equal(re[lane], ref["root_test"][f])
+    plan.close()
+
+
+# (lane counts of consecutive same-fold groups with alternating alphas): one mixed 5-lane
+# device group (2 + 3, 4 + 1), two mixed ones (3 + 4 + 3 -> [3 + 2], [2 + 3]), and a run that
+# would need three alphas in one workgroup (2 + 2 + 1), which stays one device group per alpha
+MIXES = {"2+3": [2, 3], "4+1": [4, 1], "3+4+3": [3, 4, 3], "2+2+1": [2, 2, 1]}
+
+
+@pytest.mark.parametrize("exact", [0, 1])
+@pytest.mark.parametrize("mix", sorted(MIXES))
+def test_mixed_alpha_groups_vs_oracle(eng, mix, exact, monkeypatch):
+    """Lanes of several (alpha, fold) groups of the SAME fold cut together into one device
+    group (kp_group_dev.nl2: the group's last lanes take a second (alpha, beta); the count
+    tables are shared, the logs are per alpha), as engine.fold_pieces makes them for grids
+    whose penalty count is not a multiple of the workgroup width (the 11-mer's 7): every
+    cell of every lane, the root test -2LL and the backtrack (which re-derives each lane's
+    decisions with its own alpha and fails on a mismatch) against the oracle run with that
+    lane's alpha, for the fast-log path and KP_EXACT_LOGS."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    from oracle import oracle as O
+    monkeypatch.setenv("KP_EXACT_LOGS", str(exact))
+    rng = random.Random(200 + len(mix) + exact)
+    gp, ctx = _random_case(rng, 5)
+    nf = 2
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(7), np.uint32)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr = tot_m.sum() - tot_m
+    utr = tot_u.sum() - tot_u
+    alphas = [0.5, 4.0, 1.5]
+    betas = {a: (a * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr)) for a in alphas}
+    allpens = [0.0, 1.5, 3.0, 4.5, 6.0, 8.0, 11.0]
+    groups = []
+    for f in range(nf):
+        for i, n in enumerate(MIXES[mix]):
+            a = alphas[i % len(alphas)]
+            groups.append((f, a, float(betas[a][f]), allpens[i:i + n]))
+    plan = eng.Plan(eng.get_device(0), gp, 64)
+    plan.set_counts(Mk, Uk)
+    rt, re, _ = plan.run(groups)
+    lane = 0
+    refs = {}
+    for f, a, b, pens in groups:
+        for c in pens:
+            if (a, c) not in refs:
+                refs[(a, c)] = O.cv_pass(gp, contexts, Mf, Uf, a, betas[a], c, 32)
+            ref = refs[(a, c)]
+            score, _ = plan.dump_lane(lane)
+            assert bits_equal(score, ref["score"][:, f]), (mix, f, a, c)
+            assert bits_equal(rt[lane], ref["score"][-1, f])
+            assert bits_equal(re[lane], ref["root_test"][f])
+            lane += 1
     plan.close()
 
 

@@ -105,6 +105,8 @@ def test_engine_run_groups_lane_granular_over_devices(monkeypatch):
     ran = {}
 
     class FakePlan:
+        info = {"lanes_per_workgroup": 5}  # Plan.info's piece width
+
         def __init__(self, dev):
             self.dev = dev
 
@@ -216,6 +218,8 @@ def test_engine_run_groups_fold_feed_order(monkeypatch):
     log = []
 
     class FakePlan:
+        info = {"lanes_per_workgroup": 5}  # Plan.info's piece width
+
         def __init__(self, dev):
             self.dev = dev
 
@@ -272,6 +276,8 @@ def test_engine_run_groups_gpu_named_twice(monkeypatch):
     made = []
 
     class FakePlan:
+        info = {"lanes_per_workgroup": 5}  # Plan.info's piece width
+
         def __init__(self, dev, rep):
             self.key = (dev, rep)
             made.append(self.key)
