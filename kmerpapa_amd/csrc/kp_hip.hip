@@ -755,7 +755,8 @@ static int launch_dp_hz(hipStream_t st, const kp_dp_params &P, unsigned nb, unsi
 // (the mixed builds always split: their k-mer code adds register spills at every width)
 template <typename CT, int NL, bool MIX>
 static int launch_dp(hipStream_t st, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
-    return (P.H == 0 || (NL > 3 && !MIX)) ? launch_dp_hz<CT, NL, true, MIX>(st, P, nb, ngroups, threads, lds)
+    constexpr bool one_build = NL > 3 && !MIX;  // (mixed, one build for all levels: +1-2 ms)
+    return (P.H == 0 || one_build) ? launch_dp_hz<CT, NL, true, MIX>(st, P, nb, ngroups, threads, lds)
                                 : launch_dp_hz<CT, NL, false, MIX>(st, P, nb, ngroups, threads, lds);
 }
 

@@ -207,6 +207,48 @@ int main(int argc, char **argv) {
             std::stable_sort(kv.begin(), kv.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
             const uint64_t G = 8;
             for (uint64_t q = 0; q < nb; ++q) xs[(q / G) & 7u].push_back(kv[q].second);
+        } else if (sched == "keyed") {
+            // blocks sorted by a key built from KP_SIM_KEY = comma list, slowest first, of
+            // high positions "i" (the digit) or "ci:T" (the digit's chunk, digit / T); then
+            // dealt in runs of `param` to the XCDs
+            std::vector<std::pair<int, int>> spec;  // (position, chunk size or 0; -1 = snake)
+            const char *e = getenv("KP_SIM_KEY");
+            for (const char *c = e ? e : ""; *c;) {
+                int chunk = 0;
+                if (*c == 's') {  // "si": digit order reversed when the slower key is odd
+                    chunk = -1;
+                    ++c;
+                }
+                if (*c == 'c') ++c;
+                const int pos = atoi(c);
+                while (*c >= '0' && *c <= '9') ++c;
+                if (*c == ':') {
+                    ++c;
+                    chunk = atoi(c);
+                    while (*c >= '0' && *c <= '9') ++c;
+                }
+                spec.push_back({pos, chunk});
+                while (*c == ',') ++c;
+            }
+            std::vector<std::pair<uint64_t, uint64_t>> kv(nb);
+            for (uint64_t e2 = 0; e2 < nb; ++e2) {
+                const uint64_t h = P.hlist[b0 + e2];
+                uint64_t key = 0;
+                uint64_t par = 0;
+                for (auto &sp : spec) {
+                    uint32_t d = kp_high_digit(g, h, sp.first);
+                    if (sp.second < 0) {
+                        if (par & 1u) d = g.r[g.t + sp.first] - 1 - d;
+                    } else if (sp.second > 0)
+                        d /= (uint32_t)sp.second;
+                    key = key * 16 + d;
+                    par += d;
+                }
+                kv[e2] = {key, h};
+            }
+            std::stable_sort(kv.begin(), kv.end(), [](const auto &a2, const auto &b2) { return a2.first < b2.first; });
+            const uint64_t G = (uint64_t)std::max(param, 1);
+            for (uint64_t q = 0; q < nb; ++q) xs[(q / G) & 7u].push_back(kv[q].second);
         } else {
             fprintf(stderr, "unknown schedule\n");
             return 2;
