@@ -198,6 +198,34 @@ def test_11mer_sublattice_cv_vs_oracle(eng):
     assert lanes == 70 and checked == 10
 
 
+def test_11mer_grid_fold_pieces_vs_oracle(eng):
+    """Config 5's 7x7 grid as the CV driver runs it (engine.run_groups: each fold's lanes cut
+    into 5-lane pieces, four of every seven spanning two alphas -> mixed device groups) on
+    config 5's counts restricted to AANNNMNNAAA (2.3M cells), 10 folds: the root train and
+    root test of every one of the 490 lanes equal the oracle's run with that lane's alpha
+    (the backtrack re-derives each lane's optimal tree with its own alpha)."""
+    from kmerpapa_amd.score_utils import get_betas
+    from oracle import oracle as O
+    gp = "AANNNMNNAAA"
+    ctx = _restricted("ANNNNMNNNNA", gp)
+    nf = 10
+    alphas = [0.5, 1.0, 2.0, 3.0, 5.0, 7.0, 10.0]
+    contexts, Mf, Uf, Mk, Uk, mtr, utr = _folds(ctx, gp, nf)
+    betas = {a: get_betas(a, mtr, utr) for a in alphas}
+    groups = [(f, a, float(betas[a][f]), PENS11) for a in alphas for f in range(nf)]
+    passes, _ = eng.plan_passes(groups, 7, 5)
+    assert sum(1 for p in passes if len({g[1] for g in p}) == 2) == 5 * nf  # mixed pieces
+    rt, re, _ = eng.run_groups(gp, Mk, Uk, groups, devices=eng.visible_devices()[:1])
+    for a_i, a in enumerate(alphas):
+        for p_i, c in enumerate(PENS11):
+            ref = O.cv_pass(gp, contexts, Mf, Uf, a, betas[a], c, 32, threads=_threads())
+            for f in range(nf):
+                lane = (a_i * nf + f) * len(PENS11) + p_i
+                assert bits_equal(rt[lane], ref["root_train"][f]), (a, c, f, "root train")
+                assert bits_equal(re[lane], ref["root_test"][f]), (a, c, f, "root test")
+    eng.release_all()
+
+
 def _wide_term(m, u, alpha, beta, pen):
     p = (m + alpha) / (((m + u) + alpha) + beta)
     s = pen
