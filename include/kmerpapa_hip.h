@@ -124,6 +124,13 @@ int kp_counts_fold(kp_plan *plan, int fold, const void *M_fold, const void *U_fo
 int kp_pass(kp_plan *plan, const kp_group *groups, int n_groups, float *root_train, float *root_test,
             uint64_t *n_leaves);
 int kp_last_pass_stats(const kp_plan *plan, kp_pass_stats *out);
+/* Host-only (no GPU): the workgroups ("device groups") kp_pass would run `groups` as, with
+ * `lanes_per_workgroup` lanes per workgroup (kp_plan_info): lane0[i] / nl[i] = first lane
+ * and lanes of device group i (lanes numbered group-major), nl2[i] = its trailing lanes
+ * that take a second (alpha, beta) (a mixed group of two same-fold groups; 0 = one alpha).
+ * *n_out = number of device groups; at most cap entries are written. */
+int kp_device_groups(const kp_group *groups, int n_groups, int lanes_per_workgroup, int32_t *lane0, int32_t *nl,
+                     int32_t *nl2, int cap, int *n_out);
 /* Tuning: with KP_LAUNCH_TIMES=1 in the environment, the device time (ms) of every sweep
  * launch of the last pass (lane classes in order, high levels ascending); *n = launches
  * (0 without the variable), at most cap written to ms. */

@@ -910,26 +910,10 @@ static int ensure_lanes(kp_plan *p, uint64_t lanes) {
     return KP_OK;
 }
 
-template <typename CT>
-static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *root_train, float *root_test,
-                    uint64_t *n_leaves) {
-    auto t0 = std::chrono::steady_clock::now();
-    kp_ctx *c = p->ctx;
-    const kp::host_plan &hp = p->hp;
-    kp_geom g = hp.g;
-    g.nf = p->nf;
-    // split user groups into device groups that fit two workgroups per CU in LDS when
-    // possible (LDS is the occupancy limit of the sweep)
-    const int per_wg = wg_lanes(hp, sizeof(CT), c->lds_max);
-    if (dp_lds_bytes(hp, 1, sizeof(CT)) > c->lds_max) return fail(KP_E_ARG, "block does not fit LDS");
-    for (int i = 0; i < n_groups; ++i) {
-        const kp_group &u = groups[i];
-        if (u.n_lanes < 1 || u.n_lanes > KP_GROUP_MAX_LANES) return fail(KP_E_ARG, "group lanes must be 1..8");
-        if (u.fold >= p->nf || u.fold < -1) return fail(KP_E_ARG, "fold out of range");
-        if (u.fold >= 0 && !p->fold_set[u.fold])
-            return fail(KP_E_STATE, "counts of fold " + std::to_string(u.fold) + " are not set (kp_counts_fold)");
-    }
-    std::vector<kp_group_dev> dg;
+// The device groups of a pass (host code; kp_pass, and kp_device_groups for tests): user
+// groups in order, lanes group-major, lane0 = first lane of each device group
+static void plan_device_groups(const kp_group *groups, int n_groups, int per_wg, std::vector<kp_group_dev> &dg) {
+    dg.clear();
     uint32_t lane = 0;
     // lanes [s, s + n) of the run of user groups g0.. (group-major) as one device group;
     // lanes of a second user group with another (alpha, beta) become the mixed set 2
@@ -1010,6 +994,31 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
             }
         i = e;
     }
+}
+
+template <typename CT>
+static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *root_train, float *root_test,
+                    uint64_t *n_leaves) {
+    auto t0 = std::chrono::steady_clock::now();
+    kp_ctx *c = p->ctx;
+    const kp::host_plan &hp = p->hp;
+    kp_geom g = hp.g;
+    g.nf = p->nf;
+    // split user groups into device groups that fit two workgroups per CU in LDS when
+    // possible (LDS is the occupancy limit of the sweep)
+    const int per_wg = wg_lanes(hp, sizeof(CT), c->lds_max);
+    if (dp_lds_bytes(hp, 1, sizeof(CT)) > c->lds_max) return fail(KP_E_ARG, "block does not fit LDS");
+    for (int i = 0; i < n_groups; ++i) {
+        const kp_group &u = groups[i];
+        if (u.n_lanes < 1 || u.n_lanes > KP_GROUP_MAX_LANES) return fail(KP_E_ARG, "group lanes must be 1..8");
+        if (u.fold >= p->nf || u.fold < -1) return fail(KP_E_ARG, "fold out of range");
+        if (u.fold >= 0 && !p->fold_set[u.fold])
+            return fail(KP_E_STATE, "counts of fold " + std::to_string(u.fold) + " are not set (kp_counts_fold)");
+    }
+    std::vector<kp_group_dev> dg;
+    plan_device_groups(groups, n_groups, per_wg, dg);
+    uint32_t lane = 0;
+    for (const kp_group_dev &d : dg) lane += (uint32_t)d.nl;
     const uint32_t Ltot = lane;
     g.Ltot = Ltot;
     // launch classes: device groups with equal lane counts share one launch per level
@@ -1284,6 +1293,24 @@ static int run_codes(kp_plan *p, uint32_t lane, uint8_t *code) {
 }
 
 extern "C" {
+
+int kp_device_groups(const kp_group *groups, int n_groups, int lanes_per_workgroup, int32_t *lane0, int32_t *nl,
+                     int32_t *nl2, int cap, int *n_out) {
+    if (!groups || n_groups <= 0 || !n_out || lanes_per_workgroup < 1 || lanes_per_workgroup > KP_GROUP_LANES)
+        return fail(KP_E_ARG, "bad arguments");
+    for (int i = 0; i < n_groups; ++i)
+        if (groups[i].n_lanes < 1 || groups[i].n_lanes > KP_GROUP_MAX_LANES)
+            return fail(KP_E_ARG, "group lanes must be 1..8");
+    std::vector<kp_group_dev> dg;
+    plan_device_groups(groups, n_groups, lanes_per_workgroup, dg);
+    *n_out = (int)dg.size();
+    for (int i = 0; i < (int)dg.size() && i < cap; ++i) {
+        if (lane0) lane0[i] = dg[i].lane0;
+        if (nl) nl[i] = dg[i].nl;
+        if (nl2) nl2[i] = dg[i].nl2;
+    }
+    return KP_OK;
+}
 
 int kp_pass(kp_plan *p, const kp_group *groups, int n_groups, float *root_train, float *root_test,
             uint64_t *n_leaves) {

@@ -63,7 +63,7 @@ EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_de
            "kp_plan_destroy", "kp_plan_get_info", "kp_plan_host", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
            "kp_reserve_lanes", "kp_last_pass_stats", "kp_last_launch_ms", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
            "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free",
-           "kp_format_long_rows", "kp_py_repr"]
+           "kp_format_long_rows", "kp_py_repr", "kp_device_groups"]
 
 
 def load():
@@ -101,6 +101,8 @@ def load():
         L.kp_counts_fold.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_uint64]
         L.kp_pass.argtypes = [vp, ctypes.POINTER(KPGroup), ctypes.c_int, vp, vp, vp]
         L.kp_last_pass_stats.argtypes = [vp, ctypes.POINTER(KPPassStats)]
+        L.kp_device_groups.argtypes = [ctypes.POINTER(KPGroup), ctypes.c_int, ctypes.c_int, vp, vp, vp, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int)]
         L.kp_last_launch_ms.argtypes = [vp, vp, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
         L.kp_reserve_lanes.argtypes = [vp, ctypes.c_uint32]
         L.kp_fit_leaves.argtypes = [vp, ctypes.c_uint32, vp, ctypes.c_uint64, u64p]
@@ -294,6 +296,38 @@ def plan_info(gen_pat, max_block=0):
     return {name: getattr(info, name) for name, _ in KPPlanInfo._fields_}
 
 
+def _group_array(groups):
+    """``groups`` (list of ``(fold, alpha, beta, penalties)``; ``beta`` may be a callable) as
+    the C-ABI's kp_group array; returns it and the number of lanes."""
+    arr = (KPGroup * len(groups))()
+    nl = 0
+    for i, (fold, alpha, beta, pens) in enumerate(groups):
+        pens = list(pens)
+        if not 1 <= len(pens) <= MAX_GROUP_LANES:
+            raise ValueError("a group holds 1..8 penalties")
+        arr[i].fold = int(fold)
+        arr[i].n_lanes = len(pens)
+        arr[i].alpha = float(alpha)
+        arr[i].beta = float(beta() if callable(beta) else beta)
+        for j, c in enumerate(pens):
+            arr[i].penalty[j] = float(c)
+        nl += len(pens)
+    return arr, nl
+
+
+def device_groups(groups, width):
+    """The workgroups (device groups) kp_pass runs ``groups`` as, at ``width`` lanes per
+    workgroup (kp_device_groups, host code): a list of ``(lane0, lanes, mixed_lanes)``."""
+    arr, nl = _group_array(groups)
+    cap = nl
+    lane0 = np.zeros(cap, np.int32)
+    nls = np.zeros(cap, np.int32)
+    nl2 = np.zeros(cap, np.int32)
+    n = ctypes.c_int()
+    _check(load().kp_device_groups(arr, len(groups), width, _ptr(lane0), _ptr(nls), _ptr(nl2), cap, ctypes.byref(n)))
+    return [(int(lane0[i]), int(nls[i]), int(nl2[i])) for i in range(n.value)]
+
+
 def device_count():
     n = ctypes.c_int(0)
     _check(load().kp_device_count(ctypes.byref(n)))
@@ -403,19 +437,7 @@ class Plan:
         Returns ``(root_train f32[L], root_test f32[L], n_leaves u64[L])`` with lanes
         numbered group-major.
         """
-        arr = (KPGroup * len(groups))()
-        nl = 0
-        for i, (fold, alpha, beta, pens) in enumerate(groups):
-            pens = list(pens)
-            if not 1 <= len(pens) <= MAX_GROUP_LANES:
-                raise ValueError("a group holds 1..8 penalties")
-            arr[i].fold = int(fold)
-            arr[i].n_lanes = len(pens)
-            arr[i].alpha = float(alpha)
-            arr[i].beta = float(beta() if callable(beta) else beta)
-            for j, c in enumerate(pens):
-                arr[i].penalty[j] = float(c)
-            nl += len(pens)
+        arr, nl = _group_array(groups)
         rt = np.zeros(nl, np.float32)
         re = np.zeros(nl, np.float32)
         nlv = np.zeros(nl, np.uint64)

@@ -36,5 +36,8 @@ for ci, comp in enumerate(comps):
     plan.run(groups)
     dt = time.perf_counter() - t0
     st = plan.stats()
-    print(json.dumps({"groups": comp, "mixed": ci in mixed, "lanes": sum(comp), "pass_s": round(dt, 4), "dp_ms": round(st["dp_ms"], 2),
-                      "ms_per_lane": round(st["dp_ms"] / sum(comp), 2)}), flush=True)
+    rec = {"groups": comp, "mixed": ci in mixed, "lanes": sum(comp), "pass_s": round(dt, 4), "dp_ms": round(st["dp_ms"], 2),
+           "ms_per_lane": round(st["dp_ms"] / sum(comp), 2)}
+    if os.environ.get("KP_LAUNCH_TIMES") == "1":  # per-launch device times (lane classes, high levels ascending)
+        rec["launch_ms"] = [round(x, 3) for x in plan.launch_ms()]
+    print(json.dumps(rec), flush=True)
