@@ -39,5 +39,5 @@ for ci, comp in enumerate(comps):
     rec = {"groups": comp, "mixed": ci in mixed, "lanes": sum(comp), "pass_s": round(dt, 4), "dp_ms": round(st["dp_ms"], 2),
            "ms_per_lane": round(st["dp_ms"] / sum(comp), 2)}
     if os.environ.get("KP_LAUNCH_TIMES") == "1":  # per-launch device times (lane classes, high levels ascending)
-        rec["launch_ms"] = [round(x, 3) for x in plan.launch_ms()]
+        rec["launch_ms"] = [round(float(x), 3) for x in plan.launch_ms()]
     print(json.dumps(rec), flush=True)
