@@ -433,7 +433,7 @@ __host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0,
 // 4-pair chunks, the first KP_PRE_CHUNKS already loaded into pre[] by the caller (so the
 // loads overlap the logs), the rest read from lp.  The wave runs as many chunks as its
 // longest list; shorter lists end in (B, B) pairs that read the +inf slot B.
-template <int NL, int W, bool MIX = false, typename SP>
+template <int NL, int W, bool MIX = false, int PRE = KP_PRE_CHUNKS, typename SP>
 __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, const uint4 *pre, const uint4 *lp, SP st,
                                                 const kp_single_ctx &sc, double alpha, double beta,
                                                 const double *pen, uint32_t j0 = 0) {
@@ -452,19 +452,19 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
 #ifdef KP_HALF_CHUNKS
     // a chunk whose last two pairs are padding runs as a 2-pair chunk
 #pragma unroll
-    for (int k = 0; k < KP_PRE_CHUNKS; ++k)
+    for (int k = 0; k < PRE; ++k)
         if (4u * k < npairs) {
             if (npairs - 4u * k > 2u)
                 kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
             else
                 kp_chunk_minv<NL, W, 2>(st, pre[k], j0, lmin);
         }
-    for (uint32_t k = KP_PRE_CHUNKS; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
 #else
 #pragma unroll
-    for (int k = 0; k < KP_PRE_CHUNKS; ++k)
+    for (int k = 0; k < PRE; ++k)
         if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
-    for (uint32_t k = KP_PRE_CHUNKS; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
 #endif
     kp_cell_store<W, MIX>(row, lmin, sc, pen, alpha, beta, j0);
 }

@@ -75,6 +75,9 @@ struct kp_dp_params {
 #endif
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
+#ifndef KP_NARROW_CHUNKS
+#define KP_NARROW_CHUNKS KP_PRE_CHUNKS  // pair chunks prefetched per cell on lane-split (narrow) levels
+#endif
 
 // the fast path's float64 log (kp_libm.h): kp_fast_log (fdlibm, table-free) with
 // -DKP_FAST_LOG, else the device's own (ocml)
@@ -355,9 +358,11 @@ kp_dp_kernel(kp_dp_params P) {
                 const uint32_t info = cur[0].z;
                 const uint32_t npairs = cur[0].w & 0xFFu;
                 const uint4 *lp = P.T.lpairs + (cur[0].w >> 8);
-                uint4 pre[KP_PRE_CHUNKS];
+                // narrow level: every chunk of the cell's list in flight at once (a 3-position
+                // block's top cell has 21 pairs = 6 chunks; KP_NARROW_CHUNKS A/B knob)
+                uint4 pre[KP_NARROW_CHUNKS];
 #pragma unroll
-                for (int c = 0; c < KP_PRE_CHUNKS; ++c)
+                for (int c = 0; c < KP_NARROW_CHUNKS; ++c)
                     if (4u * c < npairs) pre[c] = lp[c];
                 kp_single_ctx sc;
                 sc.exact = exact;
@@ -373,7 +378,7 @@ kp_dp_kernel(kp_dp_params P) {
                     sc.log1mp = KP_DLOG(1.0 - pr);
                 }
                 const double pj = G->pen[j];
-                kp_dp_cell_list<NL, 1>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, aj, bj, &pj, j);
+                kp_dp_cell_list<NL, 1, false, KP_NARROW_CHUNKS>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, aj, bj, &pj, j);
             }
         } else
 #pragma unroll
