@@ -94,9 +94,9 @@ struct kp_hpair {
 
 // one low cell in level order: what the level phase needs, in one 16-byte load
 struct kp_lowdesc {
-    uint16_t l;      // low cell index inside the block
-    uint16_t l1, l2; // children of its first split (count recurrence); 0xFFFF for k-mer-low cells
+    uint32_t l;      // low cell index inside the block (a whole word: the kernel uses it as loaded)
     uint16_t kl;     // k-mer-low index (k-mer-low cells only)
+    uint16_t pad_;
     uint32_t info;   // packed low digits (4 bits per position)
     uint32_t pl;     // low split pairs: (first 4-pair chunk in kp_plan's lpairs) << 8 | count
 };

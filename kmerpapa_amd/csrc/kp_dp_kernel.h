@@ -10,6 +10,7 @@
 #include "kp_core.h"
 
 #define KP_DP_MAX_THREADS 1024
+#define KP_DP_MAX_LEVELS (3 * KP_MAXT)  // low levels of a block (<= 3 per N position)
 
 // LDS-qualified element types: pointers to them are 32-bit and address LDS directly
 typedef __attribute__((address_space(3))) float kp_lds_f32;
@@ -38,6 +39,8 @@ struct kp_dp_params {
     uint64_t hbase;
     int H;
     int lmax;
+    int32_t loffv[KP_DP_MAX_LEVELS + 2];  // level offsets of the low cells (kernel arguments: scalar loads,
+                                          // not vector loads whose waits stalled every level's start)
     uint32_t ptab_entries;     // separable count table entries (kp_plan.h)
     uint32_t pscratch_entries; // largest intermediate table of its build
     int remap;  // block -> XCD mapping: G > 1 = runs of G list entries per XCD (default 8),
@@ -325,7 +328,7 @@ kp_dp_kernel(kp_dp_params P) {
     auto lane_split = [&](int cells) { return P.lanesplit && cells * NL <= nthr; };
     uint4 cur[KP_IPT], nxt[KP_IPT];
     {
-        const int beg = P.T.loff[0], cnt = P.T.loff[1] - beg;
+        const int beg = P.loffv[0], cnt = P.loffv[1] - beg;
         if (lane_split(cnt)) {
             if ((int)threadIdx.x / NL < cnt) cur[0] = desc[beg + (int)threadIdx.x / NL];
         } else {
@@ -337,9 +340,9 @@ kp_dp_kernel(kp_dp_params P) {
         }
     }
     for (int lam = 0; lam <= lmax; ++lam) {
-        const int beg = P.T.loff[lam], cnt = P.T.loff[lam + 1] - beg;
+        const int beg = P.loffv[lam], cnt = P.loffv[lam + 1] - beg;
         if (lam < lmax) {
-            const int nbeg = P.T.loff[lam + 1], ncnt = P.T.loff[lam + 2] - nbeg;
+            const int nbeg = P.loffv[lam + 1], ncnt = P.loffv[lam + 2] - nbeg;
             if (lane_split(ncnt)) {
                 if ((int)threadIdx.x / NL < ncnt) nxt[0] = desc[nbeg + (int)threadIdx.x / NL];
             } else {
@@ -354,7 +357,7 @@ kp_dp_kernel(kp_dp_params P) {
             const int q = (int)threadIdx.x / NL;
             const uint32_t j = threadIdx.x % NL;
             if (q < cnt && !KP_SKIP(P, 8)) {
-                const uint32_t l = cur[0].x & 0xFFFFu;
+                const uint32_t l = cur[0].x;
                 const uint32_t info = cur[0].z;
                 const uint32_t npairs = cur[0].w & 0xFFu;
                 const uint4 *lp = P.T.lpairs + (cur[0].w >> 8);
@@ -385,7 +388,7 @@ kp_dp_kernel(kp_dp_params P) {
         for (int k = 0; k < KP_IPT; ++k) {
             const int q = (int)threadIdx.x + k * (int)blockDim.x;
             if (q < cnt) {
-                const uint32_t l = cur[k].x & 0xFFFFu;
+                const uint32_t l = cur[k].x;
                 const uint32_t info = cur[k].z;
                 // the cell's split-pair list (plan tables, L2-resident): issued before the
                 // logs so the loads overlap them

@@ -1062,6 +1062,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.S = p->d_S;
     P.groups = p->d_groups;
     P.lmax = hp.lmax;
+    if (hp.lmax > KP_DP_MAX_LEVELS) return fail(KP_E_ARG, "too many low levels");
+    for (int l = 0; l <= hp.lmax + 1; ++l) P.loffv[l] = hp.loff[l];
     P.ptab_entries = hp.ptab_entries;
     P.pscratch_entries = hp.pscratch_entries;
 #ifdef KP_ABLATION

@@ -208,16 +208,15 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
         });
         for (uint32_t q = 0; q < B; ++q) P.lorder[q] = (uint16_t)idx[q];
     }
-    // level-ordered descriptors: first split pair (count recurrence) and k-mer-low index
+    // level-ordered descriptors: cell, k-mer-low index, digits, split-pair list
     P.ldesc.resize(B);
     P.kl2l.assign(nkl, 0);
     for (uint32_t q = 0; q < B; ++q) {
         uint32_t l = P.lorder[q];
         kp_lowdesc D;
         memset(&D, 0, sizeof(D));
-        D.l = (uint16_t)l;
+        D.l = l;
         D.info = P.lowinfo[l];
-        D.l1 = D.l2 = 0xFFFF;
         if (llev[l] == 0) {
             uint32_t kl = 0, w = 1;
             for (int i = 0; i < t; ++i) {
@@ -226,15 +225,6 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
             }
             D.kl = (uint16_t)kl;
             P.kl2l[kl] = (uint16_t)l;
-        } else {
-            for (int i = 0; i < t; ++i) {
-                uint32_t d = kp_low_digit(D.info, i);
-                if (P.tabs[i].np[d]) {
-                    D.l1 = (uint16_t)(l - (d - P.tabs[i].pa[d][0]) * (uint32_t)g.cgl[i]);
-                    D.l2 = (uint16_t)(l - (d - P.tabs[i].pb[d][0]) * (uint32_t)g.cgl[i]);
-                    break;
-                }
-            }
         }
         // the cell's low split pairs as child-cell pairs (c1 | c2 << 16), position by
         // position in scan order, padded to whole 4-pair chunks with (B, B): slot B of the
