@@ -313,8 +313,6 @@ kp_dp_kernel(kp_dp_params P) {
     // four float4 items per thread at a time, two pairs per step: 16 row loads in flight
     // per thread even when the block has few pairs (measured best of 1-4 items x 1-4 pairs)
     kp_gather_items<NL, (NL <= 3 ? 2 : 4), 2>(P, hp, np, nnt, lane0, st);
-    __syncthreads();
-    KP_STAMP(1);
 
     // ---- levels: low cells inside the block, level by level ----
     // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
@@ -326,22 +324,27 @@ kp_dp_kernel(kp_dp_params P) {
     // cell's lanes over NL threads: the same work with a 1/NL-long dependent chain
     const int nthr = (int)blockDim.x;
     auto lane_split = [&](int cells) { return P.lanesplit && cells * NL <= nthr; };
+    // the first level's descriptors, loaded without branches (threads past the level's
+    // cells load its last descriptor and never use it) and in flight across the barrier
     uint4 cur[KP_IPT], nxt[KP_IPT];
     {
-        const int beg = P.loffv[0], cnt = P.loffv[1] - beg;
-        if (lane_split(cnt)) {
-            if ((int)threadIdx.x / NL < cnt) cur[0] = desc[beg + (int)threadIdx.x / NL];
+        const int c = P.loffv[1] - P.loffv[0];
+        if (lane_split(c)) {
+            cur[0] = desc[P.loffv[0] + min((int)threadIdx.x / NL, c - 1)];
         } else {
 #pragma unroll
-            for (int k = 0; k < KP_IPT; ++k) {
-                const int q = (int)threadIdx.x + k * nthr;
-                if (q < cnt) cur[k] = desc[beg + q];
-            }
+            for (int k = 0; k < KP_IPT; ++k) cur[k] = desc[P.loffv[0] + min((int)threadIdx.x + k * nthr, c - 1)];
         }
     }
+    __syncthreads();
+    // vmcnt(0) here, before the level loop: otherwise the compiler puts the wait for these
+    // loads inside the loop body, where it also catches every level's descriptor prefetch
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    KP_STAMP(1);
+
     for (int lam = 0; lam <= lmax; ++lam) {
         const int beg = P.loffv[lam], cnt = P.loffv[lam + 1] - beg;
-        if (lam < lmax) {
+        if (lam < lmax) {  // (guarded loads here: the compiler then waits for them only at the level's end)
             const int nbeg = P.loffv[lam + 1], ncnt = P.loffv[lam + 2] - nbeg;
             if (lane_split(ncnt)) {
                 if ((int)threadIdx.x / NL < ncnt) nxt[0] = desc[nbeg + (int)threadIdx.x / NL];

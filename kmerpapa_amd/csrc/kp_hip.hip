@@ -1064,6 +1064,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     P.lmax = hp.lmax;
     if (hp.lmax > KP_DP_MAX_LEVELS) return fail(KP_E_ARG, "too many low levels");
     for (int l = 0; l <= hp.lmax + 1; ++l) P.loffv[l] = hp.loff[l];
+    for (int l = 0; l <= hp.lmax; ++l)  // (the sweep's descriptor loads assume every level holds a cell)
+        if (hp.loff[l + 1] <= hp.loff[l]) return fail(KP_E_ARG, "empty low level");
     P.ptab_entries = hp.ptab_entries;
     P.pscratch_entries = hp.pscratch_entries;
 #ifdef KP_ABLATION
