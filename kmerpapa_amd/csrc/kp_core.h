@@ -12,9 +12,11 @@
 //   S[h][lane][Bpad]  f32  train score of cell (h,l) for one lane (lane = one penalty of
 //                          one (alpha, fold) group)
 //   C[h][lane][Bpad]  u8   argmin code: (position << 3) | pair, or KP_SINGLE
-//   K[nf+1][h][kl][2] CT   counts (M, U) of the block's k-mer-low cells kl; slot 0 = all
+//   K[nf+1][q][kl][2] CT   counts (M, U) of the block's k-mer-low cells kl; slot 0 = all
 //                          data (the sum over folds), slot 1 + f = fold f (slot-major, so a
-//                          fold's table is filled and read with contiguous rows)
+//                          fold's table is filled and read with contiguous rows); rows in
+//                          the plan's block-list order q (the sweep's workgroup knows q
+//                          before it has loaded its block h; kpos[h] = q)
 //
 // Tie rule: the reference scans positions 0..k-1, pairs in table order, with a strict
 // "<" starting from +inf, then the single-pattern term with a strict "<" in float64.
@@ -152,10 +154,12 @@ __host__ __device__ inline float kp_single_test(const kp_cnt &c, double logp, do
 __host__ __device__ inline uint32_t kp_kslots(const kp_geom &g) { return (uint32_t)g.nf + 1u; }
 __host__ __device__ inline uint64_t kp_kslot_elems(const kp_geom &g) { return g.nblocks * (uint64_t)g.n_kl * 2; }
 
-// counts of one k-mer-low cell of block h for group fold f (f < 0: fit mode)
+// counts of one k-mer-low cell of the block whose count rows are row krow of K (on the
+// device the block's position in the plan's block list, kp_dev_tables.kpos) for group
+// fold f (f < 0: fit mode)
 template <typename CT>
-__host__ __device__ inline kp_cnt kp_kl_counts(const kp_geom &g, const CT *K, uint64_t h, uint32_t kl, int fold) {
-    const CT *row = K + (h * g.n_kl + kl) * 2;
+__host__ __device__ inline kp_cnt kp_kl_counts(const kp_geom &g, const CT *K, uint64_t krow, uint32_t kl, int fold) {
+    const CT *row = K + (krow * g.n_kl + kl) * 2;
     const uint64_t sm = (uint64_t)row[0], su = (uint64_t)row[1];
     kp_cnt c;
     if (fold < 0) {
@@ -480,12 +484,12 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
 // pre (optional): this thread's first row (k-mer-low cell tid), loaded by the caller ahead
 // of time so the load's latency overlaps other work.
 template <typename CT, typename LM, typename SyncFn>
-__host__ __device__ inline void kp_build_count_table(const kp_geom &g, const CT *K, uint64_t h, int fold, LM lm,
+__host__ __device__ inline void kp_build_count_table(const kp_geom &g, const CT *K, uint64_t krow, int fold, LM lm,
                                                      CT *bufA, CT *bufB, CT *ptab, uint32_t tid, uint32_t nth,
                                                      SyncFn sync, const kp_cnt *pre = nullptr) {
     CT *out0 = (g.t == 1) ? ptab : bufA;
     for (uint32_t kl = tid; kl < g.n_kl; kl += nth) {
-        const kp_cnt c = (pre && kl == tid) ? *pre : kp_kl_counts<CT>(g, K, h, kl, fold);
+        const kp_cnt c = (pre && kl == tid) ? *pre : kp_kl_counts<CT>(g, K, krow, kl, fold);
         out0[2 * kl] = (CT)c.mtr;
         out0[2 * kl + 1] = (CT)c.utr;
     }
@@ -559,14 +563,16 @@ __host__ __device__ inline bool kp_dig_is_kmer(const kp_geom &g, uint64_t dig) {
 
 // train/test counts of cell x for a group fold: K rows of its block over the matching
 // k-mer-low cells (sums are exact in itype, so any order equals the reference's)
+// (kpos: block -> count row of K; nullptr = rows in block order, the host emulator's K)
 template <typename CT>
 __host__ __device__ inline kp_cnt kp_cell_counts(const kp_geom &g, const uint32_t *klofs, const uint16_t *kllist,
-                                                 const CT *K, uint64_t x, int fold) {
+                                                 const CT *K, uint64_t x, int fold, const uint32_t *kpos = nullptr) {
     const uint64_t h = x / g.B;
+    const uint64_t krow = kpos ? (uint64_t)kpos[h] : h;
     const uint32_t l = (uint32_t)(x % g.B);
     kp_cnt c = {0, 0, 0, 0};
     for (uint32_t q = klofs[l]; q < klofs[l + 1]; ++q) {
-        const kp_cnt e = kp_kl_counts<CT>(g, K, h, kllist[q], fold);
+        const kp_cnt e = kp_kl_counts<CT>(g, K, krow, kllist[q], fold);
         c.mtr += e.mtr;
         c.utr += e.utr;
         c.mte += e.mte;

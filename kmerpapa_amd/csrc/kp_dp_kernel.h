@@ -26,6 +26,7 @@ struct kp_dev_tables {
     const kp_lowdesc *ldesc;
     const uint64_t *hdig;
     const uint64_t *hnp;
+    const uint32_t *kpos;  // block -> its position in the block list = its count row of K
     const uint8_t *lowmask;
     const uint4 *lpairs;  // low split-pair lists in 4-pair chunks (kp_plan.h lpairs)
 };
@@ -254,11 +255,13 @@ kp_dp_kernel(kp_dp_params P) {
     // this thread's k-mer-low count row (the count table's first step), loaded before the
     // high-pair setup below so that the two latencies overlap (unconditional raw loads from
     // valid rows -- a branch would make the compiler wait for them at its join -- and the
-    // subtraction after the setup)
+    // subtraction after the setup).  K's rows are in block-list order: the address needs
+    // no h, so these loads do not wait for the block-list load
+    const uint64_t krow = P.hbase + widx;
     CT kraw[4];
     {
         const uint32_t kl = threadIdx.x < g.n_kl ? threadIdx.x : 0u;
-        const CT *row = K + (h * g.n_kl + kl) * 2;
+        const CT *row = K + (krow * g.n_kl + kl) * 2;
         const CT *fr = row + kp_kslot_elems(g) * (uint64_t)(fold >= 0 ? 1 + fold : 0);
         kraw[0] = row[0];
         kraw[1] = row[1];
@@ -303,7 +306,7 @@ kp_dp_kernel(kp_dp_params P) {
     // (kp_kl_counts of the preloaded row: train = all data - fold, CV :22-24)
     const uint64_t kte_m = fold >= 0 ? (uint64_t)kraw[2] : 0, kte_u = fold >= 0 ? (uint64_t)kraw[3] : 0;
     const kp_cnt kpre = {(uint64_t)kraw[0] - kte_m, (uint64_t)kraw[1] - kte_u, kte_m, kte_u};
-    kp_build_count_table<CT>(g, K, h, fold, lm, reinterpret_cast<CT *>(smem),
+    kp_build_count_table<CT>(g, K, krow, fold, lm, reinterpret_cast<CT *>(smem),
                              reinterpret_cast<CT *>(smem) + (size_t)P.pscratch_entries * 2, ptab, threadIdx.x,
                              blockDim.x, [] { __syncthreads(); }, &kpre);
     __syncthreads();

@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables
                                                         const CT *__restrict__ Kin_M, const CT *__restrict__ Kin_U,
                                                         uint32_t ncol, uint32_t s0, CT *__restrict__ K) {
     const uint64_t h = T.hlist[hbase + blockIdx.x];
-    const uint64_t se = kp_kslot_elems(g), row = h * (uint64_t)g.n_kl * 2;
+    const uint64_t se = kp_kslot_elems(g), row = (hbase + blockIdx.x) * (uint64_t)g.n_kl * 2;  // list order
     if (H == 0) {
         // all high digits are nucleotides: the block's k-mer-low cells are k-mers
         uint64_t kbase = 0;
@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables
             break;
         }
     }
-    const uint64_t r1 = h1 * (uint64_t)g.n_kl * 2, r2 = h2 * (uint64_t)g.n_kl * 2;
+    const uint64_t r1 = (uint64_t)T.kpos[h1] * g.n_kl * 2, r2 = (uint64_t)T.kpos[h2] * g.n_kl * 2;
     for (uint32_t e = threadIdx.x; e < g.n_kl * ncol * 2; e += blockDim.x) {
         const uint32_t c = e / (2 * g.n_kl), r = e % (2 * g.n_kl);
         const uint64_t base = se * (s0 + c);
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(256) kp_bt_level(kp_bt_params P) {
         uint64_t mtr = 0, utr = 0, mte = 0, ute = 0;
         const uint32_t q0 = P.T.klofs[l], q1 = P.T.klofs[l + 1];
         for (uint32_t q = q0 + lid; q < q1; q += 64) {
-            const kp_cnt c = kp_kl_counts<CT>(g, K, h, P.T.kllist[q], fold);
+            const kp_cnt c = kp_kl_counts<CT>(g, K, P.T.kpos[h], P.T.kllist[q], fold);
             mtr += c.mtr; utr += c.utr; mte += c.mte; ute += c.ute;
         }
         kp_cnt c;
@@ -353,7 +353,7 @@ __global__ void kp_codes_kernel(kp_geom g, kp_dev_tables T, const CT *K, const f
     const uint64_t npat = g.nblocks * g.B;
     for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < npat;
          x += (uint64_t)gridDim.x * blockDim.x) {
-        const kp_cnt c = kp_cell_counts<CT>(g, T.klofs, T.kllist, K, x, G.fold);
+        const kp_cnt c = kp_cell_counts<CT>(g, T.klofs, T.kllist, K, x, G.fold, T.kpos);
         const uint64_t dig = kp_cell_digits(g, x);
         auto score = [&](uint64_t y) { return S[kp_s_off(g, y / g.B, lane, (uint32_t)(y % g.B))]; };
         float v;
@@ -405,13 +405,14 @@ struct kp_plan {
     uint32_t *d_klofs = nullptr;
     uint16_t *d_kllist = nullptr;
     uint32_t *d_hlist = nullptr;
+    uint32_t *d_kpos = nullptr;
     kp_lowdesc *d_ldesc = nullptr;
     uint64_t *d_hdig = nullptr;
     uint64_t *d_hnp = nullptr;
     uint8_t *d_lowmask = nullptr;
     uint32_t *d_lpairs = nullptr;
     // counts
-    void *d_K = nullptr;     // [h][kl][nf + 1][2] CT (kp_core.h)
+    void *d_K = nullptr;     // [nf + 1][q][kl][2] CT, rows in block-list order (kp_core.h)
     int nf = 0;
     int ct_bytes = 0;
     std::vector<uint8_t> fold_set;  // fold f's slot holds counts (kp_counts_fold / kp_set_counts)
@@ -448,6 +449,7 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     T.klofs = p->d_klofs;
     T.kllist = p->d_kllist;
     T.hlist = p->d_hlist;
+    T.kpos = p->d_kpos;
     T.ldesc = p->d_ldesc;
     T.hdig = p->d_hdig;
     T.hnp = p->d_hnp;
@@ -550,7 +552,7 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
     int rc;
     if ((rc = upload(&p->d_tabs, p->hp.tabs)) || (rc = upload(&p->d_lowinfo, p->hp.lowinfo)) ||
         (rc = upload(&p->d_loff, p->hp.loff)) || (rc = upload(&p->d_klofs, p->hp.klofs)) ||
-        (rc = upload(&p->d_kllist, p->hp.kllist)) || (rc = upload(&p->d_hlist, p->hp.hlist)) ||
+        (rc = upload(&p->d_kllist, p->hp.kllist)) || (rc = upload(&p->d_hlist, p->hp.hlist)) || (rc = upload(&p->d_kpos, p->hp.kpos)) ||
         (rc = upload(&p->d_ldesc, p->hp.ldesc)) ||
         (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_hnp, p->hp.hnp)) || (rc = upload(&p->d_lowmask, p->hp.lowmask)) ||
         (rc = upload(&p->d_lpairs, p->hp.lpairs))) {
@@ -565,7 +567,7 @@ void kp_plan_destroy(kp_plan *p) {
     if (!p) return;
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
     free_scores(p);
-    void *bufs[] = {p->d_tabs,    p->d_lowinfo, p->d_loff,   p->d_klofs,   p->d_kllist, p->d_hlist, p->d_ldesc,
+    void *bufs[] = {p->d_tabs,    p->d_lowinfo, p->d_loff,   p->d_klofs,   p->d_kllist, p->d_hlist, p->d_kpos, p->d_ldesc,
                     p->d_hdig,    p->d_hnp,     p->d_lowmask, p->d_lpairs, p->d_K,      p->d_nodes, p->d_groups,
                     p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
                     p->d_leaves};

@@ -54,6 +54,7 @@ struct host_plan {
     std::vector<uint32_t> klofs;       // [B + 1]
     std::vector<uint16_t> kllist;      // k-mer-low cells matching each low cell
     std::vector<uint32_t> hlist;       // [nblocks] blocks sorted by high level
+    std::vector<uint32_t> kpos;        // [nblocks] block -> its position in hlist (its count row)
     std::vector<uint64_t> hdig;        // [nblocks] their high digits, 4 bits per high position
     std::vector<uint64_t> hnp;         // [nblocks] their split pairs per high position, 3 bits each
     std::vector<uint64_t> hoff;        // [hmax + 2]
@@ -401,6 +402,8 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
             P.hdig[q] = w;
         }
     }
+    P.kpos.resize(g.nblocks);
+    for (uint64_t q = 0; q < g.nblocks; ++q) P.kpos[P.hlist[q]] = (uint32_t)q;
     P.hnp.resize(g.nblocks);
     for (uint64_t q = 0; q < g.nblocks; ++q) {
         uint64_t n = 0;
