@@ -79,6 +79,9 @@ struct kp_dp_params {
 #endif
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
+#ifndef KP_PS
+#define KP_PS 8  // threads per (cell, lane) on a block's narrowest levels (power of 2, <= 64)
+#endif
 #ifndef KP_NARROW_CHUNKS
 #define KP_NARROW_CHUNKS KP_PRE_CHUNKS  // pair chunks prefetched per cell on lane-split (narrow) levels
 #endif
@@ -326,14 +329,24 @@ kp_dp_kernel(kp_dp_params P) {
     // narrow levels (cells x lanes <= threads, e.g. the block's top levels) split each
     // cell's lanes over NL threads: the same work with a 1/NL-long dependent chain
     const int nthr = (int)blockDim.x;
-    auto lane_split = [&](int cells) { return P.lanesplit && cells * NL <= nthr; };
+    // threads per cell of a level: KP_PS * NL on the narrowest levels (the block's top
+    // cells: each (cell, lane) split over KP_PS threads by pair chunks, partial minima
+    // combined by wave shuffles), NL on narrow ones (one lane per thread), else 1 (KP_IPT
+    // cells per thread)
+    // (pair split only in the 1-lane build: wider builds spill with it; A/B: 1 lane 136.2 ->
+    // 134.2 ms, 3 lanes 248 -> 406, 5 lanes 380 -> 398)
+    constexpr bool kPS = NL == 1;
+    auto cell_threads = [&](int cells) {
+        return !P.lanesplit ? 1 : (kPS && cells * NL * KP_PS <= nthr) ? NL * KP_PS : cells * NL <= nthr ? NL : 1;
+    };
+    auto lane_split = [&](int cells) { return cell_threads(cells) > 1; };
     // the first level's descriptors, loaded without branches (threads past the level's
     // cells load its last descriptor and never use it) and in flight across the barrier
     uint4 cur[KP_IPT], nxt[KP_IPT];
     {
         const int c = P.loffv[1] - P.loffv[0];
         if (lane_split(c)) {
-            cur[0] = desc[P.loffv[0] + min((int)threadIdx.x / NL, c - 1)];
+            cur[0] = desc[P.loffv[0] + min((int)threadIdx.x / cell_threads(c), c - 1)];
         } else {
 #pragma unroll
             for (int k = 0; k < KP_IPT; ++k) cur[k] = desc[P.loffv[0] + min((int)threadIdx.x + k * nthr, c - 1)];
@@ -350,7 +363,8 @@ kp_dp_kernel(kp_dp_params P) {
         if (lam < lmax) {  // (guarded loads here: the compiler then waits for them only at the level's end)
             const int nbeg = P.loffv[lam + 1], ncnt = P.loffv[lam + 2] - nbeg;
             if (lane_split(ncnt)) {
-                if ((int)threadIdx.x / NL < ncnt) nxt[0] = desc[nbeg + (int)threadIdx.x / NL];
+                const int q = (int)threadIdx.x / cell_threads(ncnt);
+                if (q < ncnt) nxt[0] = desc[nbeg + q];
             } else {
 #pragma unroll
                 for (int k = 0; k < KP_IPT; ++k) {
@@ -359,7 +373,51 @@ kp_dp_kernel(kp_dp_params P) {
                 }
             }
         }
-        if (lane_split(cnt)) {
+        if (kPS && cell_threads(cnt) == NL * KP_PS) {
+          if constexpr (kPS) {
+            // each (cell, lane) on KP_PS consecutive lanes of one wave: thread r takes pair
+            // chunks r, r + KP_PS, ...; the minima meet by shuffles (min is exact in any
+            // order, NaN candidates drop out as in the sequential scan); the group's first
+            // thread adds the gathered high minimum and the single-pattern term
+            const int gi = (int)threadIdx.x / KP_PS, r = (int)threadIdx.x % KP_PS;
+            const int q = gi / NL;
+            const uint32_t j = (uint32_t)(gi % NL);
+            const bool act = q < cnt && !KP_SKIP(P, 8);
+            float part = __builtin_huge_valf();
+            if (act) {
+                const uint32_t l = cur[0].x;
+                const uint32_t npairs = cur[0].w & 0xFFu;
+                const uint4 *lp = P.T.lpairs + (cur[0].w >> 8);
+                const uint32_t nch = (npairs + 3u) >> 2;
+                for (uint32_t c = (uint32_t)r; c < nch; c += KP_PS)
+                    kp_chunk_minv<NL, 1>((kp_lds_f32 *)st, lp[c], j, &part);
+#pragma unroll
+                for (int m = 1; m < KP_PS; m <<= 1) part = fminf(part, __shfl_xor(part, m, KP_PS));
+                if (r == 0) {
+                    kp_single_ctx sc;
+                    const double aj = (MIX && (int)j >= js) ? alpha2 : alpha, bj = (MIX && (int)j >= js) ? beta2 : beta;
+                    sc.exact = exact;
+                    kp_ptab_counts<CT>(g, lm, ptab, l, cur[0].z, &sc.c.mtr, &sc.c.utr);
+                    sc.kmer = high_zero && lam == 0;
+                    sc.c.mte = sc.c.ute = 0;
+                    sc.logp = sc.log1mp = 0.0;
+                    if (!sc.kmer) {
+                        const double pr = kp_rate(sc.c, aj, bj);
+                        sc.logp = KP_DLOG(pr);
+                        sc.log1mp = KP_DLOG(1.0 - pr);
+                    }
+                    kp_lds_f32 *row = (kp_lds_f32 *)st + l * NL + j;
+                    const double pj = G->pen[j];
+                    if (sc.kmer) {
+                        row[0] = kp_kmer_train(sc.c, aj, bj, pj);
+                    } else {
+                        const float lmin = fminf(row[0], part);
+                        kp_cell_store<1>(row, &lmin, sc, &pj, aj, bj, j);
+                    }
+                }
+            }  // (act is uniform over a group's KP_PS lanes: a shuffle only reads active lanes)
+          }
+        } else if (lane_split(cnt)) {
             const int q = (int)threadIdx.x / NL;
             const uint32_t j = threadIdx.x % NL;
             if (q < cnt && !KP_SKIP(P, 8)) {
