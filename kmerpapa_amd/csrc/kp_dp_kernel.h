@@ -201,13 +201,16 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
 #ifndef KP_SMALL_WAVES
 #define KP_SMALL_WAVES 6
 #endif
+#ifndef KP_SMALL_NL
+#define KP_SMALL_NL 3  // widest group built for KP_SMALL_WAVES (A/B knob)
+#endif
 // HZ: the build that handles k-mer cells (only high level 0's blocks hold them; their
 // xlogy / xlog1py terms call the C library's logs, kp_libm.h); launches of higher levels
 // may use the build without that code (kp_hip.hip launch_dp).  MIX: the build for launch
 // classes that hold mixed groups (kp_group_dev.nl2 > 0: a second (alpha, beta) set for the
 // group's last lanes, a second pair of logs per cell); other classes use MIX = false
 template <typename CT, int NL, bool HZ, bool MIX>
-__global__ void __launch_bounds__(KP_DP_MAX_THREADS) __attribute__((amdgpu_waves_per_eu(NL <= 3 ? KP_SMALL_WAVES : 1)))
+__global__ void __launch_bounds__(KP_DP_MAX_THREADS) __attribute__((amdgpu_waves_per_eu(NL <= KP_SMALL_NL ? KP_SMALL_WAVES : 1)))
 kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const kp_geom &g = P.g;
@@ -318,7 +321,7 @@ kp_dp_kernel(kp_dp_params P) {
     // ---- gather: high-position splits, as whole child-block rows (value only) ----
     // four float4 items per thread at a time, two pairs per step: 16 row loads in flight
     // per thread even when the block has few pairs (measured best of 1-4 items x 1-4 pairs)
-    kp_gather_items<NL, (NL <= 3 ? 2 : 4), 2>(P, hp, np, nnt, lane0, st);
+    kp_gather_items<NL, (NL <= KP_SMALL_NL ? 2 : 4), 2>(P, hp, np, nnt, lane0, st);
 
     // ---- levels: low cells inside the block, level by level ----
     // one thread per cell: counts and the float64 logs once per cell for all NL lanes;
