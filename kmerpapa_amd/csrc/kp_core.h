@@ -521,7 +521,7 @@ __host__ __device__ inline void kp_build_count_table(const kp_geom &g, const CT 
 }
 
 // train counts of low cell l (packed low digits info) from the block's count table
-template <typename CT, typename LM, typename PT>
+template <typename CT, bool ALL = false, typename LM, typename PT>
 __host__ __device__ inline void kp_ptab_counts(const kp_geom &g, LM lm, PT ptab, uint32_t l, uint32_t info,
                                                uint64_t *mtr, uint64_t *utr) {
     const int tl = g.t - 1;
@@ -530,11 +530,24 @@ __host__ __device__ inline void kp_ptab_counts(const kp_geom &g, LM lm, PT ptab,
     const uint32_t m = lm[tl * 16 + dl];
     const uint32_t base = l - dl * Rl;
     CT mt = 0, ut = 0;
-    for (uint32_t c = 0; c < g.n[tl]; ++c)
-        if (m & (1u << c)) {
-            mt += ptab[2 * (base + Rl * c)];
-            ut += ptab[2 * (base + Rl * c) + 1];
+    if (ALL) {
+        // all four entries read unconditionally (in flight together, not one LDS round trip
+        // per set bit inside a branch), then masked: m has no bits at or past n[tl] <= 4
+#pragma unroll
+        for (uint32_t c = 0; c < 4; ++c) {
+            const uint32_t e = 2 * (base + Rl * (c < g.n[tl] ? c : 0u));
+            const CT a = ptab[e], b = ptab[e + 1];
+            const CT on = ((m >> c) & 1u) ? (CT)~(CT)0 : (CT)0;
+            mt += a & on;
+            ut += b & on;
         }
+    } else {
+        for (uint32_t c = 0; c < g.n[tl]; ++c)
+            if (m & (1u << c)) {
+                mt += ptab[2 * (base + Rl * c)];
+                ut += ptab[2 * (base + Rl * c) + 1];
+            }
+    }
     *mtr = (uint64_t)mt;
     *utr = (uint64_t)ut;
 }

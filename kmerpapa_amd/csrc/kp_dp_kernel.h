@@ -79,6 +79,11 @@ struct kp_dp_params {
 #endif
 
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
+// count-table reads of a cell all in flight at once (kp_ptab_counts ALL): A/B knob, see
+// profiles/r03/experiments/count_reads_ab.txt
+#ifndef KP_PTAB_ALL
+#define KP_PTAB_ALL (NL == 1)
+#endif
 #ifndef KP_PS
 #define KP_PS 8  // threads per (cell, lane) on a block's narrowest levels (power of 2, <= 64)
 #endif
@@ -93,6 +98,15 @@ struct kp_dp_params {
 #else
 #define KP_DLOG(x) log(x)
 #endif
+
+// v[j] of a small register array for a per-lane j, as a select chain (no memory access)
+template <int N>
+__device__ inline double kp_pick(const double (&v)[N], uint32_t j) {
+    double r = v[0];
+#pragma unroll
+    for (int i = 1; i < N; ++i) r = (j == (uint32_t)i) ? v[i] : r;
+    return r;
+}
 
 // a workgroup-uniform 64-bit value (read by every lane from the same LDS word) into SGPRs
 __device__ inline uint64_t kp_rfl64(uint64_t v) {
@@ -400,7 +414,7 @@ kp_dp_kernel(kp_dp_params P) {
                     kp_single_ctx sc;
                     const double aj = (MIX && (int)j >= js) ? alpha2 : alpha, bj = (MIX && (int)j >= js) ? beta2 : beta;
                     sc.exact = exact;
-                    kp_ptab_counts<CT>(g, lm, ptab, l, cur[0].z, &sc.c.mtr, &sc.c.utr);
+                    kp_ptab_counts<CT, KP_PTAB_ALL>(g, lm, ptab, l, cur[0].z, &sc.c.mtr, &sc.c.utr);
                     sc.kmer = high_zero && lam == 0;
                     sc.c.mte = sc.c.ute = 0;
                     sc.logp = sc.log1mp = 0.0;
@@ -410,7 +424,7 @@ kp_dp_kernel(kp_dp_params P) {
                         sc.log1mp = KP_DLOG(1.0 - pr);
                     }
                     kp_lds_f32 *row = (kp_lds_f32 *)st + l * NL + j;
-                    const double pj = G->pen[j];
+                    const double pj = NL <= 2 ? kp_pick(pen, j) : G->pen[j];  // (registers: 2 lanes 185 -> 179 ms; 3-5 lanes slower)
                     if (sc.kmer) {
                         row[0] = kp_kmer_train(sc.c, aj, bj, pj);
                     } else {
@@ -436,7 +450,7 @@ kp_dp_kernel(kp_dp_params P) {
                     if (4u * c < npairs) pre[c] = lp[c];
                 kp_single_ctx sc;
                 sc.exact = exact;
-                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
+                kp_ptab_counts<CT, KP_PTAB_ALL>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
                 sc.kmer = high_zero && lam == 0;
                 sc.c.mte = sc.c.ute = 0;
                 sc.logp = sc.log1mp = 0.0;
@@ -447,7 +461,7 @@ kp_dp_kernel(kp_dp_params P) {
                     sc.logp = KP_DLOG(pr);
                     sc.log1mp = KP_DLOG(1.0 - pr);
                 }
-                const double pj = G->pen[j];
+                const double pj = NL <= 2 ? kp_pick(pen, j) : G->pen[j];  // (registers: 2 lanes 185 -> 179 ms; 3-5 lanes slower)
                 kp_dp_cell_list<NL, 1, false, KP_NARROW_CHUNKS>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, aj, bj, &pj, j);
             }
         } else
@@ -468,7 +482,7 @@ kp_dp_kernel(kp_dp_params P) {
                 // counts: <= 4 table reads (the reference's M_mem/U_mem row of this cell)
                 kp_single_ctx sc;
                 sc.exact = exact;
-                kp_ptab_counts<CT>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
+                kp_ptab_counts<CT, KP_PTAB_ALL>(g, lm, ptab, l, info, &sc.c.mtr, &sc.c.utr);
                 sc.kmer = high_zero && lam == 0;
                 sc.c.mte = sc.c.ute = 0;
                 sc.logp = sc.log1mp = 0.0;
