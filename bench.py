@@ -363,6 +363,11 @@ class Shadows:
             p.wait(timeout=60)
 
 
+def note(msg):
+    """A progress line on stderr (the JSON line is stdout's only content)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def model_world(plan, prep, gen_pat, world, shadows):
     """Modelled wall-clock of the full CV on ``world`` GPUs: every rank's lane-granular share
     (shard.rank_groups) is run as that rank runs it (cv_run: its own pipelined fold split,
@@ -376,6 +381,7 @@ def model_world(plan, prep, gen_pat, world, shadows):
         shadows.go(world - 1)
         shares.append(cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], r, world)))
         shadow_s += shadows.wait(world - 1)
+        note(f"model {world} GPUs: share {r} {shares[-1]['wall_s']:.2f} s")
     return {"world": world, "share_s": [round(x["wall_s"], 4) for x in shares],
             "share_lanes": [x["lanes"] for x in shares],
             "share_passes_start_s": [round(x["passes_start_s"], 4) for x in shares],
@@ -393,6 +399,7 @@ def full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds=(2, 4, 8)):
     also models the wall-clock of a job on 2, 4 and 8 GPUs (model_world)."""
     from kmerpapa_amd.shard import rank_groups
     out = cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], rank, world))
+    note(f"full CV (rank {rank} of {world}) {out['wall_s']:.2f} s")
     out["hbm_alloc_s"] = prep["t_alloc"]
     out["wall_s_incl_alloc"] = out["wall_s"] + prep["t_alloc"]
     if world == 1 and model_worlds:
@@ -487,6 +494,7 @@ def main():
     t_end = time.perf_counter()
     barrier()
     elapsed = max_over_ranks(t_end - t_start)
+    note(f"{a.steps} timed steps {elapsed / a.steps * 1e3:.1f} ms/step")
 
     # BASELINE.json's second metric: the full grid CV wall-clock (fold split, count tables,
     # passes, root read-out), max over ranks; at N=1 also the modelled 8-GPU wall-clock
@@ -572,6 +580,7 @@ def main():
                 line["cv_full_grid_wall_s_model_8gpu"] = cv["models"]["8"]["wall_s"]
                 line["cv_full_grid_speedup_model_8gpu"] = cv["models"]["8"]["speedup"]
         if not a.no_cpu_baseline and world == 1:
+            note("cpu baseline")
             line["cpu_baseline"] = cpu_baseline(prep)
         else:
             line["cpu_baseline"] = None
