@@ -247,15 +247,15 @@ def cv_shares(prep, world, cap, width=None):
 
 
 def cv_run(plan, prep, gen_pat, groups):
-    """One job's CV work as the CV driver runs it (cv_roots with the engine): all-data
-    counts in k-mer order, the fold split drawn on a host thread and handed over fold by
-    fold (CV_tools.fold_stream -> engine.FoldFeed), the plan's table build beside it (a
+    """One job's CV work as the CV driver runs it (cv_roots with the engine): the fold
+    split drawn on a host thread and handed over fold by fold, the all-data counts in k-mer
+    order computed beside fold 0's draw (CV_tools.fold_feed -> engine.FoldFeed), the plan's table build beside it (a
     second build, timed), then ``groups``' passes in fold order, each fold uploaded when
     it arrives (engine.run_groups).  Lane buffers are already allocated (the one-time
     allocation is reported separately).  Returns the wall-clock and its parts."""
     import threading
-    from kmerpapa_amd.CV_tools import all_counts, fold_stream
-    nf, itype, nk = prep["nfolds"], prep["itype"], plan.info["n_kmers"]
+    from kmerpapa_amd.CV_tools import fold_feed
+    nf, itype = prep["nfolds"], prep["itype"]
     box = {}
     t0 = time.perf_counter()
 
@@ -264,35 +264,22 @@ def cv_run(plan, prep, gen_pat, groups):
         box["t_tables"] = time.perf_counter() - t0
     th = threading.Thread(target=tables)
     th.start()
-    contexts, Ma, Ua = all_counts(prep["ctx"], itype)
-    idx = engine.kmer_order(gen_pat, contexts)
-    M_all = np.zeros(nk, itype)
-    U_all = np.zeros(nk, itype)
-    M_all[idx] = Ma
-    U_all[idx] = Ua
-    feed = engine.FoldFeed(M_all, U_all, nf)
-
-    def produce():
-        try:
-            for f, Mf, Uf in fold_stream(prep["ctx"], nf, np.random.RandomState(1), itype):
-                mk = np.zeros(nk, itype)
-                uk = np.zeros(nk, itype)
-                mk[idx] = Mf
-                uk[idx] = Uf
-                feed.put(f, mk, uk)
-                box.setdefault("t_fold", []).append(time.perf_counter() - t0)
-        except BaseException as e:
-            feed.fail(e)
-    pr = threading.Thread(target=produce)
-    pr.start()
+    feed, pr = fold_feed(prep["ctx"], gen_pat, nf, np.random.RandomState(1), itype)
     th.join()
     t_start = time.perf_counter() - t0
-    engine.run_groups(gen_pat, feed, None, groups, devices=[plan.device.device])
+    engine.PASS_LOG = log = []
+    try:
+        engine.run_groups(gen_pat, feed, None, groups, devices=[plan.device.device])
+    finally:
+        engine.PASS_LOG = None
     pr.join()
     wall = time.perf_counter() - t0
     box["p"].close()
-    return {"wall_s": wall, "plan_tables_s": box["t_tables"], "fold_ready_s": [round(x, 4) for x in box["t_fold"]],
-            "fold_split_s": box["t_fold"][-1], "passes_start_s": t_start, "lanes": sum(len(g[3]) for g in groups)}
+    fold_t = [t - t0 for t in feed.t_put]
+    return {"wall_s": wall, "plan_tables_s": box["t_tables"], "fold_ready_s": [round(x, 4) for x in fold_t],
+            "fold_split_s": fold_t[-1], "passes_start_s": t_start, "lanes": sum(len(g[3]) for g in groups),
+            # per pass: lanes, [counts wait + upload, start, end] in s from the job's start
+            "passes": [[n, round(w, 4), round(a - t0, 4), round(b - t0, 4)] for _, n, w, a, b in log]}
 
 
 def shadow_host_side(prep, gen_pat):
@@ -386,6 +373,8 @@ def model_world(plan, prep, gen_pat, world, shadows):
             "share_lanes": [x["lanes"] for x in shares],
             "share_passes_start_s": [round(x["passes_start_s"], 4) for x in shares],
             "share_fold_split_s": [round(x["fold_split_s"], 4) for x in shares],
+            "share_fold0_s": [x["fold_ready_s"][0] for x in shares],
+            "share_passes": [x["passes"] for x in shares],
             "shadow_host_side_s": [round(min(shadow_s), 4), round(max(shadow_s), 4)] if shadow_s else None,
             "wall_s": max(x["wall_s"] for x in shares)}
 

@@ -9,6 +9,8 @@ The device path never sees the ``[npat, nf]`` arrays of the reference (a 9-mer l
 has 7.7e9 rows): :func:`fold_tables` returns only the per-k-mer fold counts, which the
 C-ABI uploads (``kp_set_counts``).
 """
+import threading
+
 import numpy as np
 
 from .pattern_utils import PatternEnumeration, generality, matches
@@ -117,6 +119,53 @@ def fold_stream(contextD, n_folds, prng, itype=np.uint64):
         col -= s
         yield f, s[:nk].astype(itype), s[nk:].astype(itype)
     yield n_folds - 1, col[:nk].astype(itype), col[nk:].astype(itype)
+
+
+def fold_feed(contextD, gen_pat, n_folds, prng, itype=np.uint64, on_done=None):
+    """Start the pipelined fold split of the CV driver: returns ``(feed, thread)``, an
+    engine.FoldFeed that receives fold f's counts in k-mer order as soon as
+    :func:`fold_stream` has drawn it, and the producer thread (the caller joins it).  The
+    draws start first: the all-data counts and the k-mer order, which only the scatter into
+    k-mer order needs, are computed beside fold 0's draw (the native sampler drops the
+    GIL), so fold 0 arrives one k-mer ordering earlier.  ``on_done()`` runs after the last
+    fold.  Same draws from the same stream as :func:`fold_tables`."""
+    from . import engine
+    nk = generality(gen_pat)
+    box = {}
+    ready = threading.Event()
+
+    def produce():
+        try:
+            for f, Mf, Uf in fold_stream(contextD, n_folds, prng, itype):
+                ready.wait()
+                if "feed" not in box:  # the caller's side failed and raises its own error
+                    return
+                mk = np.zeros(nk, itype)
+                uk = np.zeros(nk, itype)
+                mk[box["idx"]] = Mf
+                uk[box["idx"]] = Uf
+                box["feed"].put(f, mk, uk)
+            if on_done is not None:
+                on_done()
+        except BaseException as e:  # the GPU side raises it from feed.get
+            ready.wait()
+            if "feed" in box:
+                box["feed"].fail(e)
+
+    th = threading.Thread(target=produce)
+    th.start()
+    try:
+        contexts, Ma, Ua = all_counts(contextD, itype)
+        idx = engine.kmer_order(gen_pat, contexts if hasattr(contexts, "letters") else list(contexts))
+        M_all = np.zeros(nk, itype)
+        U_all = np.zeros(nk, itype)
+        M_all[idx] = Ma
+        U_all[idx] = Ua
+        box["idx"] = idx
+        box["feed"] = engine.FoldFeed(M_all, U_all, n_folds)
+    finally:
+        ready.set()
+    return box["feed"], th
 
 
 def make_all_folds_contextD_patterns(contextD, U_mem, M_mem, general_pattern, prng, itype=np.uint64):

@@ -19,7 +19,7 @@ import threading
 import numpy as np
 
 from .. import engine
-from ..CV_tools import all_counts, fold_stream, fold_tables
+from ..CV_tools import fold_feed, fold_tables
 from ..pattern_utils import code, generality, pattern_level, perm_code
 from ..score_utils import get_betas
 from ..shard import fold_order
@@ -95,28 +95,9 @@ def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, ity
         producer = None
         try:
             if pipelined:
-                contexts, Ma, Ua = all_counts(contextD, itype)
-                idx = engine.kmer_order(gen_pat, contexts if hasattr(contexts, "letters") else list(contexts))
-                M_all = np.zeros(n_kmers, itype)
-                U_all = np.zeros(n_kmers, itype)
-                M_all[idx] = Ma
-                U_all[idx] = Ua
-                feed = engine.FoldFeed(M_all, U_all, nfolds)
-
-                def _produce(feed=feed, idx=idx):
-                    try:
-                        for f, Mf, Uf in fold_stream(contextD, nfolds, prng, itype):
-                            mk = np.zeros(n_kmers, itype)
-                            uk = np.zeros(n_kmers, itype)
-                            mk[idx] = Mf
-                            uk[idx] = Uf
-                            feed.put(f, mk, uk)
-                        if verbose > 0:
-                            print('CV sampling DONE', file=sys.stderr)
-                    except BaseException as e:  # the GPU side raises it from feed.get
-                        feed.fail(e)
-                producer = threading.Thread(target=_produce)
-                producer.start()
+                done = (lambda: print('CV sampling DONE', file=sys.stderr)) if verbose > 0 else None
+                feed, producer = fold_feed(contextD, gen_pat, nfolds, prng, itype, on_done=done)
+                M_all, U_all = feed.M_all, feed.U_all
                 M_tot = M_all.sum(dtype=np.uint64) + carryM.sum(dtype=np.uint64)  # = M_sum.sum()
                 U_tot = U_all.sum(dtype=np.uint64) + carryU.sum(dtype=np.uint64)
                 counts_M, counts_U = feed, None

@@ -80,6 +80,53 @@ inline double loggam(double x) {
     return gl;
 }
 
+// loggam of whole numbers (every argument the sampler passes is one, >= 1), four at a time:
+// the small ones -- a k-mer's count and the draws from it -- from a table of loggam's own
+// values (bit-identical by construction, and it skips the up-to-seven logs loggam spends
+// below 7); the large ones run loggam's own operations side by side (the same IEEE
+// operations in the same order per argument, so the same bits, without one argument's
+// 10-step polynomial waiting on the previous one's).
+struct loggam_table {
+    enum { N = 8192 };
+    double v[N];
+    loggam_table() {
+        v[0] = 0.0;
+        for (int i = 1; i < N; ++i) v[i] = loggam((double)i);
+    }
+};
+
+inline double loggam_sum4(int64_t k0, int64_t k1, int64_t k2, int64_t k3) {
+    static const loggam_table t;
+    static const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03, 7.936507936507937e-04,
+                                 -5.952380952380952e-04, 8.417508417508418e-04, -1.917526917526918e-03,
+                                 6.410256410256410e-03, -2.955065359477124e-02, 1.796443723688307e-01,
+                                 -1.39243221690590e+00};
+    const int64_t k[4] = {k0, k1, k2, k3};
+    double r[4], x0[4], gl0[4], x2[4];
+    bool big[4];
+    for (int j = 0; j < 4; ++j) {
+        big[j] = !((uint64_t)(k[j] - 1) < (uint64_t)(loggam_table::N - 1));
+        x0[j] = big[j] ? (double)k[j] : 8.0;  // >= 7 for every argument that takes this path
+        x2[j] = (1.0 / x0[j]) * (1.0 / x0[j]);
+        gl0[j] = a[9];
+    }
+    for (int i = 8; i >= 0; --i)
+        for (int j = 0; j < 4; ++j) {
+            gl0[j] *= x2[j];
+            gl0[j] += a[i];
+        }
+    for (int j = 0; j < 4; ++j) {
+        if (!big[j]) {
+            r[j] = t.v[k[j]];
+        } else if (k[j] < 7) {  // k <= 0: loggam's own path (never taken by the sampler)
+            r[j] = loggam((double)k[j]);
+        } else {
+            r[j] = gl0[j] / x0[j] + 0.5 * 1.8378770664093453e+00 + (x0[j] - 0.5) * log(x0[j]) - x0[j];
+        }
+    }
+    return ((r[0] + r[1]) + r[2]) + r[3];
+}
+
 inline int64_t hypergeometric_hyp(mt19937 &rng, int64_t good, int64_t bad, int64_t sample) {
     const int64_t d1 = bad + good - sample;
     const double d2 = (double)(bad < good ? bad : good);
@@ -108,8 +155,7 @@ inline int64_t hypergeometric_hrua(mt19937 &rng, int64_t good, int64_t bad, int6
     const double d7 = sqrt((double)(popsize - m) * sample * d4 * d5 / (popsize - 1) + 0.5);
     const double d8 = D1 * d7 + D2;
     const int64_t d9 = (int64_t)floor((double)(m + 1) * (mingoodbad + 1) / (popsize + 2));
-    const double d10 = (loggam(d9 + 1) + loggam(mingoodbad - d9 + 1) + loggam(m - d9 + 1) +
-                        loggam(maxgoodbad - m + d9 + 1));
+    const double d10 = loggam_sum4(d9 + 1, mingoodbad - d9 + 1, m - d9 + 1, maxgoodbad - m + d9 + 1);
     const double mm = (double)(m < mingoodbad ? m : mingoodbad) + 1.0, fl = floor(d6 + 16 * d7);
     const double d11 = mm < fl ? mm : fl;
     int64_t Z;
@@ -119,8 +165,7 @@ inline int64_t hypergeometric_hrua(mt19937 &rng, int64_t good, int64_t bad, int6
         const double W = d6 + d8 * (Y - 0.5) / X;
         if (W < 0.0 || W >= d11) continue;  // fast rejection
         Z = (int64_t)floor(W);
-        const double T = d10 - (loggam(Z + 1) + loggam(mingoodbad - Z + 1) + loggam(m - Z + 1) +
-                                loggam(maxgoodbad - m + Z + 1));
+        const double T = d10 - loggam_sum4(Z + 1, mingoodbad - Z + 1, m - Z + 1, maxgoodbad - m + Z + 1);
         if ((X * (4.0 - X) - 3.0) <= T) break;  // fast acceptance
         if (X * (X - T) >= 1) continue;         // fast rejection
         if (2.0 * log(X) <= T) break;           // accept

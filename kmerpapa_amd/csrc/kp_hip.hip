@@ -51,18 +51,28 @@
 
 // Fills count slots s0 .. s0+ncol-1 of every block of high level H.  Kin_M/Kin_U are
 // [n_kmers][ncol] (k-mer order): column c goes to slot s0 + c.  K is slot-major
-// (kp_core.h), so a block's rows of one slot are n_kl contiguous (M, U) pairs.
+// (kp_core.h), so a block's rows of one slot are n_kl contiguous (M, U) pairs.  A
+// workgroup fills KP_CROWS blocks' rows, KP_CTPR threads per row: a row is only 2 n_kl
+// counts (512 B at 9-mers) behind a chain of dependent index loads (block list, digits,
+// child rows), so one row per workgroup left the launch latency-bound (2.55 ms per fold
+// table at 9-mers).
+#define KP_CTPR 32
+#define KP_CROWS (256 / KP_CTPR)
 template <typename CT>
-__global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables T, uint64_t hbase, int H,
-                                                        const CT *__restrict__ Kin_M, const CT *__restrict__ Kin_U,
-                                                        uint32_t ncol, uint32_t s0, CT *__restrict__ K) {
-    const uint64_t h = T.hlist[hbase + blockIdx.x];
-    const uint64_t se = kp_kslot_elems(g), row = (hbase + blockIdx.x) * (uint64_t)g.n_kl * 2;  // list order
+__global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables T, uint64_t hbase, uint64_t nb,
+                                                        int H, const CT *__restrict__ Kin_M,
+                                                        const CT *__restrict__ Kin_U, uint32_t ncol, uint32_t s0,
+                                                        CT *__restrict__ K) {
+    const uint64_t q = (uint64_t)blockIdx.x * KP_CROWS + threadIdx.x / KP_CTPR;
+    if (q >= nb) return;
+    const uint32_t lt = threadIdx.x % KP_CTPR;
+    const uint64_t h = T.hlist[hbase + q];
+    const uint64_t se = kp_kslot_elems(g), row = (hbase + q) * (uint64_t)g.n_kl * 2;  // list order
     if (H == 0) {
         // all high digits are nucleotides: the block's k-mer-low cells are k-mers
         uint64_t kbase = 0;
         for (int i = 0; i < g.kh; ++i) kbase += (uint64_t)kp_high_digit(g, h, i) * g.khw[i];
-        for (uint32_t e = threadIdx.x; e < g.n_kl * ncol; e += blockDim.x) {
+        for (uint32_t e = lt; e < g.n_kl * ncol; e += KP_CTPR) {
             const uint32_t c = e / g.n_kl, kl = e % g.n_kl;
             const uint64_t src = (kbase + kl) * (uint64_t)ncol + c;
             CT *dst = K + se * (s0 + c) + row + 2 * kl;
@@ -84,7 +94,7 @@ __global__ void __launch_bounds__(256) kp_counts_kernel(kp_geom g, kp_dev_tables
         }
     }
     const uint64_t r1 = (uint64_t)T.kpos[h1] * g.n_kl * 2, r2 = (uint64_t)T.kpos[h2] * g.n_kl * 2;
-    for (uint32_t e = threadIdx.x; e < g.n_kl * ncol * 2; e += blockDim.x) {
+    for (uint32_t e = lt; e < g.n_kl * ncol * 2; e += KP_CTPR) {
         const uint32_t c = e / (2 * g.n_kl), r = e % (2 * g.n_kl);
         const uint64_t base = se * (s0 + c);
         K[base + row + r] = K[base + r1 + r] + K[base + r2 + r];
@@ -416,6 +426,15 @@ struct kp_plan {
     int nf = 0;
     int ct_bytes = 0;
     std::vector<uint8_t> fold_set;  // fold f's slot holds counts (kp_counts_fold / kp_set_counts)
+    // kp_counts_fold runs asynchronously on a stream of its own (a fold's table fills while
+    // the previous fold's pass runs): pinned + device staging of one fold's counts, the
+    // event that frees the pinned copy, and per fold the event its passes wait for
+    hipStream_t cstream = nullptr;
+    void *h_stage = nullptr, *d_stage = nullptr;
+    size_t stage_bytes = 0;
+    hipEvent_t stage_ev = nullptr;
+    std::vector<hipEvent_t> fold_ev;
+    std::vector<uint8_t> fold_async;  // fold f's table was filled on cstream (passes wait on fold_ev[f])
     // lanes
     float *d_S = nullptr;
     bool S_pool = false;  // d_S came from the device's stream-ordered pool (see alloc_scores)
@@ -571,7 +590,13 @@ void kp_plan_destroy(kp_plan *p) {
                     p->d_hdig,    p->d_hnp,     p->d_lowmask, p->d_lpairs, p->d_K,      p->d_nodes, p->d_groups,
                     p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
                     p->d_leaves};
+    if (p->cstream) (void)hipStreamSynchronize(p->cstream);
     for (void *b : bufs) dfree(b);
+    dfree(p->d_stage);
+    if (p->h_stage) (void)hipHostFree(p->h_stage);
+    if (p->stage_ev) (void)hipEventDestroy(p->stage_ev);
+    for (hipEvent_t e : p->fold_ev) (void)hipEventDestroy(e);
+    if (p->cstream) (void)hipStreamDestroy(p->cstream);
     for (hipEvent_t e : p->lev) (void)hipEventDestroy(e);
     delete p;
 }
@@ -618,6 +643,7 @@ int kp_plan_host(const char *gen_pat, uint32_t max_block, kp_plan_info *o) {
 template <typename CT>
 static int counts_alloc(kp_plan *p, int nf) {
     const kp_geom &g = p->hp.g;
+    if (p->cstream) KP_HIP(hipStreamSynchronize(p->cstream));  // no fold fill still writing the old tables
     size_t kbytes = g.nblocks * (size_t)g.n_kl * (nf + 1) * 2 * sizeof(CT);
     if (p->d_K && (p->nf != nf || p->ct_bytes != (int)sizeof(CT))) {
         dfree(p->d_K);
@@ -632,34 +658,79 @@ static int counts_alloc(kp_plan *p, int nf) {
     p->nf = nf;
     p->ct_bytes = (int)sizeof(CT);
     p->fold_set.assign(nf, 0);
+    p->fold_async.assign(nf, 0);
+    while ((int)p->fold_ev.size() < nf) {
+        hipEvent_t e = nullptr;
+        KP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        p->fold_ev.push_back(e);
+    }
     return KP_OK;
 }
 
 // Fill slots s0 .. s0+ncol-1 from [n_kmers][ncol] host arrays (one launch per high level:
 // a level's aggregated rows sum two rows of lower levels).
 template <typename CT>
-static int counts_fill(kp_plan *p, const void *M, const void *U, uint32_t ncol, uint32_t s0) {
-    kp_ctx *c = p->ctx;
+static void counts_launch(kp_plan *p, hipStream_t st, const CT *dM, const CT *dU, uint32_t ncol, uint32_t s0,
+                          hipError_t &e) {
     kp_geom g = p->hp.g;
     g.nf = p->nf;
+    kp_dev_tables T = tables_of(p);
+    for (int H = 0; H <= p->hp.hmax && e == hipSuccess; ++H) {
+        uint64_t nb = p->hp.hoff[H + 1] - p->hp.hoff[H];
+        if (!nb) continue;
+        hipLaunchKernelGGL(kp_counts_kernel<CT>, dim3((unsigned)((nb + KP_CROWS - 1) / KP_CROWS)), dim3(256), 0, st, g,
+                           T, p->hp.hoff[H], nb, H, dM, dU, ncol, s0, reinterpret_cast<CT *>(p->d_K));
+        e = hipGetLastError();
+    }
+}
+
+template <typename CT>
+static int counts_fill(kp_plan *p, const void *M, const void *U, uint32_t ncol, uint32_t s0) {
+    kp_ctx *c = p->ctx;
     const size_t in_bytes = p->hp.n_kmers * (size_t)ncol * sizeof(CT);
     CT *dM = nullptr, *dU = nullptr;
     KP_HIP(dmalloc(&dM, in_bytes));
     KP_HIP(dmalloc(&dU, in_bytes));
     hipError_t e = hipMemcpyAsync(dM, M, in_bytes, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(dU, U, in_bytes, hipMemcpyHostToDevice, c->stream);
-    kp_dev_tables T = tables_of(p);
-    for (int H = 0; H <= p->hp.hmax && e == hipSuccess; ++H) {
-        uint64_t nb = p->hp.hoff[H + 1] - p->hp.hoff[H];
-        if (!nb) continue;
-        hipLaunchKernelGGL(kp_counts_kernel<CT>, dim3((unsigned)nb), dim3(256), 0, c->stream, g, T, p->hp.hoff[H], H,
-                           dM, dU, ncol, s0, reinterpret_cast<CT *>(p->d_K));
-        e = hipGetLastError();
-    }
+    counts_launch<CT>(p, c->stream, dM, dU, ncol, s0, e);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dfree(dM);
     dfree(dU);
     if (e != hipSuccess) return fail(KP_E_HIP, std::string("count tables: ") + hipGetErrorString(e));
+    return KP_OK;
+}
+
+// One fold's table, asynchronously on the plan's count stream: the counts are copied into
+// pinned staging (once the previous fold's upload has left it), uploaded and aggregated on
+// cstream, and fold_ev[fold] marks the end; run_pass makes the pass's stream wait for it.
+template <typename CT>
+static int counts_fill_async(kp_plan *p, int fold, const void *M, const void *U) {
+    const size_t in_bytes = p->hp.n_kmers * sizeof(CT);
+    if (!p->cstream) KP_HIP(hipStreamCreateWithFlags(&p->cstream, hipStreamNonBlocking));
+    if (!p->stage_ev) KP_HIP(hipEventCreateWithFlags(&p->stage_ev, hipEventDisableTiming));
+    if (p->stage_bytes < 2 * in_bytes) {
+        KP_HIP(hipStreamSynchronize(p->cstream));
+        dfree(p->d_stage);
+        p->d_stage = nullptr;
+        if (p->h_stage) KP_HIP(hipHostFree(p->h_stage));
+        p->h_stage = nullptr;
+        p->stage_bytes = 0;
+        KP_HIP(hipHostMalloc(&p->h_stage, 2 * in_bytes, hipHostMallocDefault));
+        KP_HIP(dmalloc(&p->d_stage, 2 * in_bytes));
+        p->stage_bytes = 2 * in_bytes;
+    }
+    KP_HIP(hipEventSynchronize(p->stage_ev));  // the previous upload has left the pinned copy
+    char *h = static_cast<char *>(p->h_stage);
+    memcpy(h, M, in_bytes);
+    memcpy(h + in_bytes, U, in_bytes);
+    CT *dM = static_cast<CT *>(p->d_stage), *dU = dM + p->hp.n_kmers;
+    hipError_t e = hipMemcpyAsync(dM, h, 2 * in_bytes, hipMemcpyHostToDevice, p->cstream);
+    if (e == hipSuccess) e = hipEventRecord(p->stage_ev, p->cstream);
+    counts_launch<CT>(p, p->cstream, dM, dU, 1, 1u + (uint32_t)fold, e);
+    if (e == hipSuccess) e = hipEventRecord(p->fold_ev[fold], p->cstream);
+    if (e != hipSuccess) return fail(KP_E_HIP, std::string("fold count table: ") + hipGetErrorString(e));
+    p->fold_async[fold] = 1;
     return KP_OK;
 }
 
@@ -719,8 +790,8 @@ int kp_counts_fold(kp_plan *p, int fold, const void *M_fold, const void *U_fold,
         return fail(KP_E_ARG, "n_kmers " + std::to_string(n_kmers) + " != " + std::to_string(p->hp.n_kmers));
     if (fold < 0 || fold >= p->nf) return fail(KP_E_ARG, "fold out of range");
     KP_HIP(hipSetDevice(p->ctx->device));
-    int rc = p->ct_bytes == 4 ? counts_fill<uint32_t>(p, M_fold, U_fold, 1, 1u + (uint32_t)fold)
-                              : counts_fill<uint64_t>(p, M_fold, U_fold, 1, 1u + (uint32_t)fold);
+    int rc = p->ct_bytes == 4 ? counts_fill_async<uint32_t>(p, fold, M_fold, U_fold)
+                              : counts_fill_async<uint64_t>(p, fold, M_fold, U_fold);
     if (rc == KP_OK) p->fold_set[fold] = 1;
     return rc;
 }
@@ -1017,6 +1088,9 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         if (u.fold >= 0 && !p->fold_set[u.fold])
             return fail(KP_E_STATE, "counts of fold " + std::to_string(u.fold) + " are not set (kp_counts_fold)");
     }
+    for (int i = 0; i < n_groups; ++i)  // folds whose tables are still filling on the count stream
+        if (groups[i].fold >= 0 && p->fold_async[groups[i].fold])
+            KP_HIP(hipStreamWaitEvent(c->stream, p->fold_ev[groups[i].fold], 0));
     std::vector<kp_group_dev> dg;
     plan_device_groups(groups, n_groups, per_wg, dg);
     uint32_t lane = 0;

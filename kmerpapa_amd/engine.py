@@ -17,6 +17,7 @@ import atexit
 import ctypes
 import os
 import threading
+import time
 
 import numpy as np
 
@@ -560,6 +561,7 @@ class FoldFeed:
         self.U_all = np.ascontiguousarray(U_all, dtype=self.M_all.dtype).reshape(-1)
         self.nf = int(nf)
         self._cols = [None] * self.nf
+        self.t_put = [None] * self.nf  # perf_counter() at each fold's arrival
         self._err = None
         self._cv = threading.Condition()
 
@@ -567,6 +569,7 @@ class FoldFeed:
         with self._cv:
             self._cols[fold] = (np.ascontiguousarray(M_fold, dtype=self.M_all.dtype),
                                 np.ascontiguousarray(U_fold, dtype=self.M_all.dtype))
+            self.t_put[fold] = time.perf_counter()
             self._cv.notify_all()
 
     def fail(self, exc):
@@ -799,6 +802,9 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0):
         th.join()
 
 
+PASS_LOG = None  # a list to receive one timing record per pass of run_groups (bench.py)
+
+
 def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     """Run every lane group over the lattice of ``gen_pat`` on the given GPUs.
 
@@ -836,13 +842,44 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
                                             plan.info["lanes_per_workgroup"])
                 plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))  # one allocation
                 outs = []
-                have = set()
-                for pas in passes:
+                queued = {}
+                if feed is not None:
+                    # a feeder thread queues each fold's count table (kp_counts_fold: the
+                    # device's count stream) as soon as the fold is drawn, so it fills while
+                    # the previous fold's passes run; a pass waits until its folds are queued
+                    need = []
+                    for pas in passes:
+                        need += sorted({g[0] for g in pas if g[0] >= 0} - set(need))
+                    queued = {f: threading.Event() for f in need}
+                    fed_err = []
+
+                    def feeder():
+                        try:
+                            for f in need:
+                                plan.counts_fold(f, *feed.get(f))
+                                queued[f].set()
+                        except BaseException as e:  # raised by the pass loop below
+                            fed_err.append(e)
+                        finally:
+                            for ev in queued.values():
+                                ev.set()
+                    fth = threading.Thread(target=feeder)
+                    fth.start()
+                try:
+                    for pas in passes:
+                        t_wait = time.perf_counter()
+                        for f in sorted({g[0] for g in pas if g[0] in queued}):
+                            queued[f].wait()
+                            if fed_err:
+                                raise fed_err[0]
+                        t_run = time.perf_counter()
+                        outs.append(plan.run(pas))
+                        if PASS_LOG is not None:  # (slot, lanes, counts wait s, pass start, pass end)
+                            PASS_LOG.append((slot, sum(len(g[3]) for g in pas), t_run - t_wait, t_run,
+                                             time.perf_counter()))
+                finally:
                     if feed is not None:
-                        for f in sorted({g[0] for g in pas if g[0] >= 0} - have):
-                            plan.counts_fold(f, *feed.get(f))
-                            have.add(f)
-                    outs.append(plan.run(pas))
+                        fth.join()
             if outs:
                 results[slot] = tuple(unpermute_lanes(order, np.concatenate([o[i] for o in outs]))
                                       for i in range(3))

@@ -17,7 +17,7 @@ def _pair(colors, nf, seed, itype=np.uint64):
     return a, b, s1, s2
 
 
-@pytest.mark.parametrize("kind", range(5))
+@pytest.mark.parametrize("kind", range(6))
 def test_fold_split_matches_numpy_stream(kind):
     rng = np.random.RandomState(100 + kind)
     for trial in range(60):
@@ -30,8 +30,10 @@ def test_fold_split_matches_numpy_stream(kind):
             colors = rng.randint(0, 2 ** 31, size=n) // (1 + rng.randint(0, 1000, size=n))
         elif kind == 3:
             colors = np.where(rng.rand(n) < 0.4, 0, rng.randint(0, 10 ** 7, size=n))
-        else:
+        elif kind == 4:
             colors = rng.randint(0, 2 ** 33, size=n)      # > 2^32 totals (uint64 itype)
+        else:
+            colors = rng.randint(7800, 8600, size=n)      # loggam arguments either side of its table
         nf = int(rng.randint(1, 8))
         a, b, s1, s2 = _pair(colors, nf, int(rng.randint(0, 2 ** 31)))
         assert np.array_equal(a, b), (kind, trial)
