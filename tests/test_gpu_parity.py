@@ -709,3 +709,36 @@ def test_negative_penalty_takes_exact_logs(eng):
             score, _ = plan.dump_lane(f * len(pens) + pi)
             assert np.array_equal(score.view(np.uint32), ref["score"][:, f].view(np.uint32)), (c, f)
     plan.close()
+
+
+def test_fold_tables_fill_beside_passes(eng):
+    """kp_counts_fold is asynchronous (the plan's count stream, one event per fold that the
+    fold's passes wait on) and engine.run_groups queues each fold from a feeder thread as it
+    arrives, so fold f + 1's table fills while fold f's pass runs.  With folds arriving
+    15 ms apart over 25 ms passes, the roots equal those of the all-folds-at-once upload
+    (kp_set_counts), bit for bit."""
+    import threading
+    import time
+    from kmerpapa_amd.pattern_utils import generality
+    gp, nf = "NNNNMNNN", 4
+    rng = np.random.RandomState(11)
+    nk = generality(gp)
+    Mk = rng.randint(0, 60, size=(nk, nf)).astype(np.uint32)
+    Uk = rng.randint(60, 2000, size=(nk, nf)).astype(np.uint32)
+    groups = [(f, a, 1.0 + 0.1 * f + 0.01 * a, [2.0, 3.0, 4.0, 5.0, 6.0]) for a in (1.0, 3.0) for f in range(nf)]
+    plan = eng.get_plan(0, gp)
+    plan.set_counts(Mk, Uk)
+    want = plan.run(groups)
+    feed = eng.FoldFeed(Mk.sum(axis=1, dtype=np.uint32), Uk.sum(axis=1, dtype=np.uint32), nf)
+
+    def produce():
+        for f in range(nf):
+            time.sleep(0.015)
+            feed.put(f, Mk[:, f].copy(), Uk[:, f].copy())
+    th = threading.Thread(target=produce)
+    th.start()
+    got = eng.run_groups(gp, feed, None, groups, devices=[0])
+    th.join()
+    for w, g in zip(want[:2], got[:2]):
+        assert bits_equal(g, w)
+    assert np.array_equal(want[2], got[2])
