@@ -112,8 +112,11 @@ int kp_set_counts(kp_plan *plan, const void *M, const void *U, uint64_t n_kmers,
  * later folds (the CV driver's pipelined fold split).  kp_counts_begin: M_all, U_all
  * [n_kmers] = counts of all data (the sum of the folds to come; the train counts of fold f
  * are all data minus fold f, CV :22-24); it discards any fold set before.
- * kp_counts_fold: M_fold, U_fold [n_kmers] = fold `fold`'s counts.  kp_pass refuses a
- * group whose fold has not been set (KP_E_STATE). */
+ * kp_counts_fold: M_fold, U_fold [n_kmers] = fold `fold`'s counts; asynchronous (the
+ * counts are copied before it returns, the table fills on the plan's count stream, and
+ * every later device read of it waits for that on the device), so it may be called from
+ * another host thread while a kp_pass of another fold runs.  kp_pass refuses a group
+ * whose fold has not been set (KP_E_STATE). */
 int kp_counts_begin(kp_plan *plan, const void *M_all, const void *U_all, uint64_t n_kmers, int nf, int itype_bytes);
 int kp_counts_fold(kp_plan *plan, int fold, const void *M_fold, const void *U_fold, uint64_t n_kmers);
 

@@ -1361,6 +1361,8 @@ static int run_codes(kp_plan *p, uint32_t lane, uint8_t *code) {
     const double pen = G.pen[lane - (uint32_t)G.lane0];
     uint8_t *d_code = nullptr;
     KP_HIP(dmalloc(&d_code, hp.npat));
+    for (int f = 0; f < p->nf; ++f)  // a fold table refilled since the pass may still be filling
+        if (p->fold_async[f]) KP_HIP(hipStreamWaitEvent(c->stream, p->fold_ev[f], 0));
     const unsigned nb = (unsigned)std::min<uint64_t>((hp.npat + 255) / 256, 65535);
     hipLaunchKernelGGL(kp_codes_kernel<CT>, dim3(nb), dim3(256), 0, c->stream, g, tables_of(p),
                        reinterpret_cast<const CT *>(p->d_K), p->d_S, G, lane, pen, d_code);
