@@ -1,4 +1,4 @@
-"""Multi-rank sharding of the CV grid (kmerpapa_amd.shard), world_size 2 over gloo on the
+"""Multi-rank sharding of the CV grid (kmerpapa_amd.shard), world_size 2 and 8 over gloo on the
 CPU, with the host emulator of the blocked DP standing in for the GPU: the sharded CV
 driver must return exactly the single-process roots, every group run exactly once."""
 import os
@@ -68,7 +68,10 @@ def _work(rank, world, q):
         q.put((rank, res["train"].tobytes(), res["test"].tobytes(), ran))
 
 
-def test_two_rank_gloo_cv_matches_single_process():
+@pytest.mark.parametrize("world", [2, 8])
+def test_gloo_ranks_cv_matches_single_process(world):
+    """world_size 2 and 8 over gloo (the 8-GPU job's rank count): each rank runs its
+    lane-granular share, the all-gathered roots equal the single-process run's bytes."""
     import multiprocessing as mp
     from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
     from tests.emu import emu as E
@@ -79,7 +82,7 @@ def test_two_rank_gloo_cv_matches_single_process():
     ctxm = mp.get_context("spawn")
     q = ctxm.Queue()
     port = _free_port()
-    procs = [ctxm.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctxm.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     outs = [q.get(timeout=120) for _ in procs]
@@ -92,8 +95,8 @@ def test_two_rank_gloo_cv_matches_single_process():
         assert tr == ref["train"].tobytes() and te == ref["test"].tobytes(), f"rank {rank} roots differ"
         ran_all.extend(ran)
     want = [(f, a, p) for a in c["alphas"] for f in range(c["nfolds"]) for p in c["penalties"]]
-    assert sorted(ran_all) == sorted(want)  # every lane (alpha, fold, penalty) exactly once over both ranks
-    assert all(len(r) > 0 for _, _, _, r in outs)  # both ranks did work
+    assert sorted(ran_all) == sorted(want)  # every lane (alpha, fold, penalty) exactly once over the ranks
+    assert all(len(r) > 0 for _, _, _, r in outs)  # every rank did work (20 lanes over <= 8 ranks)
 
 
 def test_engine_run_groups_lane_granular_over_devices(monkeypatch):
