@@ -170,6 +170,17 @@ int kp_math_log(kp_ctx *ctx, const double *x, double *y, uint64_t n);
  * fdlibm log), computed on the context's GPU. */
 int kp_math_libm(kp_ctx *ctx, const double *x, double *y, uint64_t n, int fn);
 
+/* --score all_kmers on the context's GPU: one rate per k-mer, no lattice DP
+ * (src/kmerpapa/algorithms/all_kmers_CV.py: test_folds :8-13 and the k-mer loop :36-46).
+ * M, U: [n][nf] uint64 fold counts, rows in the reference's matches(gen_pat) order; per
+ * alpha a (alphas[na]) and fold f, with betas[a][f] (get_betas of the fold-train totals):
+ *   sum_train[a][f] = sum over rows i of test_folds(trM, trU, trM, trU, alpha_a, beta_af)
+ *   sum_test[a][f]  = sum over rows i of test_folds(trM, trU, M[i][f], U[i][f], alpha_a, beta_af)
+ * trM = sum_g M[i][g] - M[i][f] (likewise trU); each sum in float64, row by row from 0.0,
+ * as the reference's `sum_train += ...` loop; xlogy / xlog1py with the C library's logs. */
+int kp_allkmers_cv(kp_ctx *ctx, const uint64_t *M, const uint64_t *U, uint64_t n, int nf, const double *alphas,
+                   const double *betas, int na, double *sum_train, double *sum_test);
+
 /* Host-only (no GPU needed): the cross-validation fold split of CV_tools.py
  * make_all_folds_contextD_patterns :44-57 / sample :5-27 with numpy's legacy
  * RandomState stream.  mt_key[624] / *mt_pos = the MT19937 state of the caller's

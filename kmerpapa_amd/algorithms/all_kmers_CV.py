@@ -2,33 +2,29 @@
 reference's ``kmerpapa.algorithms.all_kmers_CV`` (src/kmerpapa/algorithms/all_kmers_CV.py,
 v0.2.4; ``--score all_kmers``).
 
-There is no lattice DP here: every k-mer is its own pattern, so the per-k-mer test
--2LL is a closed form.  The fold split is the shared one (CV_tools, native
-``kp_fold_split``); the loss is evaluated for all k-mers at once with numpy, keeping
-the reference's operation order and its sequential float64 accumulation over k-mers
-(``sum_test += ...`` in ``matches`` order, :36-41), so results are bit-identical.
+There is no lattice DP here: every k-mer is its own pattern, so the per-k-mer -2LL is a
+closed form.  The fold split is the shared one (CV_tools, native ``kp_fold_split``); the
+losses of all (k-mer, fold) pairs of every pseudo count are evaluated on the GPU
+(``kp_allkmers_cv``, csrc/kp_allk.h) with the reference's operation order and the C
+library's logs, and summed k-mer by k-mer in float64 in ``matches`` order as the
+reference's ``sum_test += ...`` loop does (:36-44), so results are bit-identical.
 """
 import sys
 
 import numpy as np
 
+from .. import engine
 from ..CV_tools import make_all_folds_contextD_kmers
 from ..pattern_utils import generality
 from ..score_utils import get_betas
 
 
 def test_folds(trainM, trainU, testM, testU, alphas, betas):
-    """-2 LL of test counts under the training rate (ref :8-13)."""
+    """-2 LL of test counts under the training rate (ref :8-13; host helper kept for the
+    reference's API -- the CV below evaluates it on the GPU)."""
     from scipy.special import xlog1py, xlogy  # (imported on use: the CLI starts 0.2 s faster without it)
     p = (trainM + alphas) / (trainM + trainU + alphas + betas)
     return -2 * (xlogy(testM, p) + xlog1py(testU, -p))
-
-
-def _seq_sum_rows(terms):
-    """Row-by-row float64 sum from 0.0, in order (what ``s += row`` does in a loop)."""
-    if terms.shape[0] == 0:
-        return np.zeros(terms.shape[1])
-    return np.add.accumulate(terms, axis=0)[-1] + 0.0
 
 
 def all_kmers(gen_pat, contextD, alphas, args, nmut, nunmut, index_mut=0):
@@ -42,6 +38,7 @@ def all_kmers(gen_pat, contextD, alphas, args, nmut, nunmut, index_mut=0):
     train_loss = {a_i: [] for a_i in range(len(alphas))}
     if index_mut != 0:
         contextD = {k: (v[index_mut], v[-1]) for k, v in contextD.items()}
+    dev = engine.get_device(engine.visible_devices()[0])  # no CPU path: raises without the library / a GPU
     prng = np.random.RandomState(args.seed)
     for _ in range(nit):
         make_all_folds_contextD_kmers(contextD, U_mem, M_mem, gen_pat, prng)
@@ -49,15 +46,11 @@ def all_kmers(gen_pat, contextD, alphas, args, nmut, nunmut, index_mut=0):
         U_sum_test = U_mem.sum(axis=0)
         M_sum_train = sum(M_sum_test) - M_sum_test
         U_sum_train = sum(U_sum_test) - U_sum_test
-        # per k-mer train counts: row total minus the fold (uint64, as the reference)
-        M_train = M_mem.sum(axis=1, keepdims=True) - M_mem
-        U_train = U_mem.sum(axis=1, keepdims=True) - U_mem
-        for a_i, alpha in enumerate(alphas):
-            betas = get_betas(alpha, M_sum_train, U_sum_train)
-            sum_train = _seq_sum_rows(test_folds(M_train, U_train, M_train, U_train, alpha, betas))
-            sum_test = _seq_sum_rows(test_folds(M_train, U_train, M_mem, U_mem, alpha, betas))
-            train_loss[a_i].extend(list(sum_train))
-            test_loss[a_i].extend(list(sum_test))
+        betas = np.array([get_betas(alpha, M_sum_train, U_sum_train) for alpha in alphas], np.float64)
+        sum_train, sum_test = dev.allkmers_cv(M_mem, U_mem, alphas, betas.reshape(len(alphas), nf))
+        for a_i in range(len(alphas)):
+            train_loss[a_i].extend(list(sum_train[a_i]))
+            test_loss[a_i].extend(list(sum_test[a_i]))
     best_test_loss = 1e100
     best_alpha = None
     for a_i, alpha in enumerate(alphas):

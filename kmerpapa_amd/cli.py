@@ -5,7 +5,7 @@ The flow: read counts -> penalty presets -> general pattern (LCA) + zero fill ->
 (optional) grid cross-validation on the GPU -> final fit on the GPU -> partition table.
 Out of scope in this build (SURVEY.md §2): ``--greedy``, ``--greedyCV`` and ``--BayesOpt``;
 they are accepted by the parser and rejected with a message.  ``--score all_kmers`` (one
-rate per k-mer, no lattice DP) runs on the host (algorithms/all_kmers_CV.py).
+rate per k-mer, no lattice DP) evaluates its loss terms on the GPU (algorithms/all_kmers_CV.py, kp_allkmers_cv).
 """
 import argparse
 import json

@@ -23,6 +23,9 @@
 //                      kp_bt_finish sums the test -2LL along the tree in float32 (CV
 //                      :158-163) and lists the leaves in the reference's order (Fit :17-24)
 //   kp_codes_kernel  : argmin code of every cell (parity dumps only)
+//   kp_allk_terms / kp_allk_sums : --score all_kmers (kp_allk.h; all_kmers_CV.py :8-46):
+//                      every (k-mer, fold) term in parallel, then the reference's
+//                      sequential float64 sum over k-mers, one thread per column
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -36,6 +39,7 @@
 #include <vector>
 
 #include "../../include/kmerpapa_hip.h"
+#include "kp_allk.h"
 #include "kp_core.h"
 #include "kp_dp_kernel.h"
 #include "kp_folds.h"
@@ -1516,6 +1520,58 @@ int kp_math_libm(kp_ctx *c, const double *x, double *y, uint64_t n, int fn) {
     dfree(dx);
     dfree(dy);
     if (e != hipSuccess) return fail(KP_E_HIP, std::string("kp_math_libm: ") + hipGetErrorString(e));
+    return KP_OK;
+}
+
+int kp_allkmers_cv(kp_ctx *c, const uint64_t *M, const uint64_t *U, uint64_t n, int nf, const double *alphas,
+                   const double *betas, int na, double *sum_train, double *sum_test) {
+    if (!c || nf < 1 || na < 0 || (n && (!M || !U)) || (na && (!alphas || !betas || !sum_train || !sum_test)))
+        return fail(KP_E_ARG, "kp_allkmers_cv: bad arguments");
+    if (!na) return KP_OK;
+    if (!n) {  // no k-mers: every sum is the reference's numpy.zeros(nf)
+        for (int a = 0; a < na; ++a)
+            for (int f = 0; f < nf; ++f) sum_train[a * nf + f] = sum_test[a * nf + f] = 0.0;
+        return KP_OK;
+    }
+    KP_HIP(hipSetDevice(c->device));
+    const size_t cnt_bytes = n * (size_t)nf * sizeof(uint64_t);
+    uint64_t *dM = nullptr, *dU = nullptr;
+    double *dB = nullptr, *dT = nullptr, *dS = nullptr;
+    hipError_t e = dmalloc(&dM, cnt_bytes);
+    if (e == hipSuccess) e = dmalloc(&dU, cnt_bytes);
+    if (e == hipSuccess) e = dmalloc(&dB, (size_t)na * nf * sizeof(double));
+    if (e == hipSuccess) e = dmalloc(&dT, 2 * (size_t)nf * n * sizeof(double));  // one alpha's terms at a time
+    if (e == hipSuccess) e = dmalloc(&dS, (size_t)na * 2 * nf * sizeof(double));
+    if (e == hipSuccess) e = hipMemcpyAsync(dM, M, cnt_bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(dU, U, cnt_bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(dB, betas, (size_t)na * nf * sizeof(double), hipMemcpyHostToDevice, c->stream);
+    const uint64_t items = n * (uint64_t)nf;
+    const unsigned nb = (unsigned)std::min<uint64_t>((items + 255) / 256, 8192);
+    for (int a = 0; a < na && e == hipSuccess; ++a) {
+        hipLaunchKernelGGL(kp_allk_terms, dim3(nb), dim3(256), 0, c->stream, dM, dU, n, nf, alphas[a],
+                           dB + (size_t)a * nf, dT);
+        e = hipGetLastError();
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(kp_allk_sums, dim3((2 * nf + 63) / 64), dim3(64), 0, c->stream, dT, n, 2 * nf,
+                               dS + (size_t)a * 2 * nf);
+            e = hipGetLastError();
+        }
+    }
+    std::vector<double> hs((size_t)na * 2 * nf);
+    if (e == hipSuccess) e = hipMemcpyAsync(hs.data(), dS, hs.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree(dM);
+    dfree(dU);
+    dfree(dB);
+    dfree(dT);
+    dfree(dS);
+    if (e != hipSuccess) return fail(KP_E_HIP, std::string("kp_allkmers_cv: ") + hipGetErrorString(e));
+    for (int a = 0; a < na; ++a)
+        for (int f = 0; f < nf; ++f) {
+            sum_train[a * nf + f] = hs[((size_t)a * 2 + 0) * nf + f];
+            sum_test[a * nf + f] = hs[((size_t)a * 2 + 1) * nf + f];
+        }
     return KP_OK;
 }
 

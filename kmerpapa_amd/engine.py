@@ -64,7 +64,7 @@ EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_de
            "kp_plan_destroy", "kp_plan_get_info", "kp_plan_host", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
            "kp_reserve_lanes", "kp_last_pass_stats", "kp_last_launch_ms", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
            "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free",
-           "kp_format_long_rows", "kp_py_repr", "kp_device_groups"]
+           "kp_format_long_rows", "kp_py_repr", "kp_device_groups", "kp_allkmers_cv"]
 
 
 def load():
@@ -117,6 +117,7 @@ def load():
         L.kp_format_long_rows.argtypes = [vp, ctypes.c_int, vp, vp, vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp,
                                           ctypes.c_uint64, u64p]
         L.kp_py_repr.argtypes = [vp, ctypes.c_uint64, vp, ctypes.c_uint64, u64p]
+        L.kp_allkmers_cv.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp, vp, ctypes.c_int, vp, vp]
         L.kp_fold_sample.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), vp, ctypes.c_uint64, ctypes.c_uint64, vp]
         for name in EXPORTS:
             if not hasattr(L, name):
@@ -370,6 +371,23 @@ class Device:
         y = np.empty_like(x)
         _check(load().kp_math_libm(self._h, _ptr(x), _ptr(y), ctypes.c_uint64(x.size), int(fn)))
         return y
+
+    def allkmers_cv(self, M, U, alphas, betas):
+        """--score all_kmers on this GPU (kp_allkmers_cv; all_kmers_CV.py :8-46): ``M``/``U``
+        ``[n, nf]`` fold counts (rows in matches(gen_pat) order), ``betas`` ``[na, nf]``.
+        Returns ``(sum_train, sum_test)`` ``[na, nf]`` float64, each summed k-mer by k-mer
+        as the reference does."""
+        M = np.ascontiguousarray(M, dtype=np.uint64)
+        U = np.ascontiguousarray(U, dtype=np.uint64)
+        if M.ndim != 2 or U.shape != M.shape:
+            raise ValueError("counts must be [n_kmers, nfolds]")
+        al = np.ascontiguousarray(alphas, dtype=np.float64).reshape(-1)
+        be = np.ascontiguousarray(betas, dtype=np.float64).reshape(al.size, M.shape[1])
+        tr = np.zeros(be.shape, np.float64)
+        te = np.zeros(be.shape, np.float64)
+        _check(load().kp_allkmers_cv(self._h, _ptr(M), _ptr(U), ctypes.c_uint64(M.shape[0]), int(M.shape[1]),
+                                     _ptr(al), _ptr(be), int(al.size), _ptr(tr), _ptr(te)))
+        return tr, te
 
     def close(self):
         if self._h:

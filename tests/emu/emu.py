@@ -72,3 +72,65 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
 
 
 run_groups.fold_feed = True
+
+
+class EmuPlan:
+    """Stand-in for ``engine.Plan`` backed by the emulator (CPU tests only): the same
+    count-upload interface (set_counts, or counts_begin + counts_fold one fold at a time,
+    as kp_counts_begin / kp_counts_fold) and ``run(groups)`` returning per-lane roots, so
+    engine.run_groups' real plan / fold-feed / pass-packing code runs unchanged.  Like the
+    device's slot-major count tables (slot 0 = all data, slot 1 + f = fold f), a group of
+    fold f sees train = all data - fold f and test = fold f."""
+
+    def __init__(self, gen_pat, max_block=0, width=5, fit=7):
+        from kmerpapa_amd.pattern_utils import generality, pattern_max
+        self.gen_pat = gen_pat
+        self.max_block = max_block or 4096
+        self.info = {"lanes_per_workgroup": width, "npat": pattern_max(gen_pat), "n_kmers": generality(gen_pat)}
+        self.fit = fit
+        self.all = None
+        self.folds = {}
+        self.reserved = 0
+        self.passes = []
+
+    def set_counts(self, M, U):
+        M = np.asarray(M)
+        U = np.asarray(U, dtype=M.dtype)
+        if M.ndim == 1:
+            M, U = M.reshape(-1, 1), U.reshape(-1, 1)
+        self.all = (M.sum(axis=1, dtype=M.dtype), U.sum(axis=1, dtype=M.dtype))
+        self.folds = {f: (M[:, f].copy(), U[:, f].copy()) for f in range(M.shape[1])}
+
+    def counts_begin(self, M_all, U_all, nf):
+        self.all = (np.asarray(M_all).copy(), np.asarray(U_all, dtype=np.asarray(M_all).dtype).copy())
+        self.folds = {}
+
+    def counts_fold(self, fold, M_fold, U_fold):
+        dt = self.all[0].dtype
+        self.folds[fold] = (np.asarray(M_fold, dt).copy(), np.asarray(U_fold, dt).copy())
+
+    def lanes_that_fit(self):
+        return self.fit
+
+    def reserve(self, lanes):
+        self.reserved = max(self.reserved, int(lanes))
+
+    def run(self, groups):
+        rt, re, nl = [], [], []
+        lanes = 0
+        for f, a, b, pens in groups:
+            if f not in self.folds:
+                raise RuntimeError(f"fold {f} has not been uploaded")  # kp_pass: KP_E_STATE
+            b = float(b() if callable(b) else b)
+            mf, uf = self.folds[f]
+            M2 = np.stack([mf, self.all[0] - mf], axis=1)
+            U2 = np.stack([uf, self.all[1] - uf], axis=1)
+            out = run(self.gen_pat, M2, U2, [(0, a, b, list(pens))], max_block=self.max_block)
+            rt.append(out["root_train"])
+            re.append(out["root_test"])
+            nl.append(out["n_leaves"])
+            lanes += len(pens)
+        if lanes > max(self.reserved, self.fit):
+            raise RuntimeError("pass wider than the reserved lane buffers")
+        self.passes.append([(g[0], g[1], len(g[3])) for g in groups])
+        return np.concatenate(rt), np.concatenate(re), np.concatenate(nl)

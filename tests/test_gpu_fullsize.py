@@ -324,3 +324,108 @@ def test_9mer_full_lane_buffer_grow_sequence(cv_split):
                 assert bits_equal(plan.gather_cells(j, cells), ref[c]), (len(pens), c)
     finally:
         plan.close()
+
+
+# ---------------------------------------------------------------------------------------
+# The same embedded-sub-lattice check through the product's own asynchronous count path:
+# the fold split drawn fold by fold on a host thread (CV_tools.fold_feed -> engine.FoldFeed),
+# the all-data counts uploaded first and the fold's table filled on the plan's count stream
+# (kp_counts_begin / kp_counts_fold), the pass run by engine.run_groups -- exactly as the
+# CV driver runs it (bottum_up_array_penalty_plus_pseudo_CV.cv_roots).
+# ---------------------------------------------------------------------------------------
+
+def _fed_pass_vs_oracle(gen_pat, ctx, nf, groups, subs):
+    """Run ``groups`` (one fold, at most one workgroup of lanes) over the whole lattice of
+    ``gen_pat`` through the fold feed; then every cell of each embedded sub-lattice in
+    ``subs`` equals the oracle's run on that sub-lattice with the full run's fold counts and
+    each lane's own (alpha, beta, c), bit for bit."""
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.CV_tools import fold_feed, fold_tables
+    from oracle import oracle as O
+    from tests.fixtures import bits_equal
+    fold = groups[0][0]
+    assert all(g[0] == fold for g in groups)
+    dev = engine.visible_devices()[0]
+    engine.release_all()
+    feed, pr = fold_feed(ctx, gen_pat, nf, np.random.RandomState(1), np.uint32)
+    try:
+        engine.run_groups(gen_pat, feed, None, groups, devices=[dev])
+    finally:
+        pr.join()
+    plan = engine.get_plan(dev, gen_pat, 0)
+    assert plan.stats()["units"] == plan.info["npat"] * sum(len(g[3]) for g in groups)  # one pass, every lane
+    # the oracle's inputs: the same seeded split drawn at once (sorted-context order); the
+    # feed's fold-f table (k-mer order) must hold exactly these counts
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(1), np.uint32)
+    idx = engine.kmer_order(gen_pat, contexts)
+    mk, uk = feed.get(fold)
+    assert np.array_equal(mk[idx], Mf[:, fold]) and np.array_equal(uk[idx], Uf[:, fold])
+    lanes = [(g[1], g[2], c) for g in groups for c in g[3]]
+    for sub in subs:
+        keep = [i for i, c in enumerate(contexts) if all(c[j] in IUPAC[ch] for j, ch in enumerate(sub))]
+        ctxs = [contexts[i] for i in keep]
+        mf, uf = Mf[keep], Uf[keep]
+        m2 = np.stack([mf[:, fold], mf.sum(axis=1) - mf[:, fold]], axis=1)
+        u2 = np.stack([uf[:, fold], uf.sum(axis=1) - uf[:, fold]], axis=1)
+        cells = _embedded_cells(gen_pat, sub)
+        assert cells.size == O.npat(sub)
+        for lane, (a, b, c) in enumerate(lanes):
+            ref = O.cv_pass(sub, ctxs, m2, u2, a, [b, b], c, 32, threads=_threads())
+            got = plan.gather_cells(lane, cells)
+            assert bits_equal(got, ref["score"][:, 0]), (sub, lane, a, c, int(np.sum(
+                got.view(np.uint32) != ref["score"][:, 0].view(np.uint32))))
+            del ref
+    return plan
+
+
+@pytest.mark.timeout(1200)
+def test_9mer_full_fold0_group_fold_feed_vs_oracle(counts):
+    """A second (alpha, fold) group of the headline pass, fold 0 (the first drawn, which
+    every share's first pass waits for), through the fold feed: every cell of ANNNMNNNA and
+    AANNMNNNV in all 5 lanes equals the oracle."""
+    from kmerpapa_amd.score_utils import get_betas
+    kmers, M, U = counts
+    ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
+    from kmerpapa_amd.CV_tools import fold_tables
+    _, Mf, Uf = fold_tables(ctx, 5, np.random.RandomState(1), np.uint32)
+    ms, us = Mf.sum(axis=0, dtype=np.uint64), Uf.sum(axis=0, dtype=np.uint64)
+    alpha = 0.5
+    b0 = float(get_betas(alpha, ms.sum() - ms, us.sum() - us)[0])
+    plan = _fed_pass_vs_oracle(GEN_PAT, ctx, 5, [(0, alpha, b0, [3.0, 4.0, 5.0, 6.0, 7.0])], SUBS)
+    assert plan.stats()["dp_launches"] == 17
+    from kmerpapa_amd import engine
+    engine.release_all()
+
+
+SUBS11 = ["AANNNMNNNAA",   # low in the index space (3.4e7 cells)
+          "AAANNMNNNVA"]   # V at the last ambiguous position: cells past 2^32 (1.6e7 cells)
+ALPHAS11 = [0.5, 1.0, 2.0, 3.0, 5.0, 7.0, 10.0]
+PENS11 = [2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0]
+
+
+@pytest.mark.timeout(1500)
+def test_11mer_full_mixed_fold_piece_fold_feed_vs_oracle():
+    """BASELINE configs[4] at full size (ANNNNMNNNNA, 7.69e9 cells, 10 folds): one MIXED
+    5-lane fold piece of the 7x7 grid exactly as engine.plan_passes cuts it (fold 6: alpha
+    3.0 with c = 6, 7, 8 and alpha 5.0 with c = 2, 3 in one workgroup, a second rate and
+    pair of logs per cell for the last two lanes), fed fold by fold as the CV driver does:
+    every cell of AANNNMNNNAA and AAANNMNNNVA (offsets past 2^32) in all 5 lanes equals the
+    oracle run with that lane's own alpha and beta."""
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.score_utils import get_betas
+    import bench
+    gp, nf, fold = "ANNNNMNNNNA", 10, 6
+    kmers, M, U = bench.synthetic_counts(gp, seed=9)
+    ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
+    _, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(1), np.uint32)
+    ms, us = Mf.sum(axis=0, dtype=np.uint64), Uf.sum(axis=0, dtype=np.uint64)
+    betas = {a: get_betas(a, ms.sum() - ms, us.sum() - us) for a in ALPHAS11}
+    grid = [(f, a, float(betas[a][f]), PENS11) for a in ALPHAS11 for f in range(nf)]
+    piece = [(fold, 3.0, float(betas[3.0][fold]), [6.0, 7.0, 8.0]), (fold, 5.0, float(betas[5.0][fold]), [2.0, 3.0])]
+    passes, _ = engine.plan_passes(grid, 7, 5)
+    assert [tuple((g[0], g[1], g[2], list(g[3])) for g in p) for p in passes].count(
+        tuple((g[0], g[1], g[2], list(g[3])) for g in piece)) == 1  # a pass of the grid's own plan
+    assert engine.device_groups(piece, 5) == [(0, 5, 2)]  # one workgroup, last 2 lanes on the second alpha
+    _fed_pass_vs_oracle(gp, ctx, nf, piece, SUBS11)
+    engine.release_all()

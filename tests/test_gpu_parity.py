@@ -111,19 +111,27 @@ def test_grid5_roots_per_fold(eng):
 def test_grid5_multi_device_path_on_one_gpu(eng, monkeypatch):
     """The single-process multi-GPU path (engine.run_groups: lane-granular slots, one host
     thread, context and HIP stream per slot, fold-by-fold count upload) run on the one GPU
-    of the box by naming it 2 and 3 times: per-fold roots and the CVfile equal the
-    reference's (config 2)."""
+    of the box by naming it 2, 3 and 8 times (8 contexts, 8 streams, 8 host threads: the
+    8-GPU job's fan-out): per-fold roots equal the oracle's and the reference's, and the
+    CVfile and best point the reference's (config 2)."""
     from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    from kmerpapa_amd.CV_tools import fold_tables
+    from oracle import oracle as O
     g = golden_json("grid5.json")
     ctx, gp, nm, nu = context_table(5)
-    for devs in ([0, 0], [0, 0, 0]):
+    contexts, Mf, Uf = fold_tables(ctx, 5, np.random.RandomState(1), np.uint32)
+    for devs in ([0, 0], [0, 0, 0], [0] * 8):
         res = cvm.cv_roots(gp, ctx, g["alphas"], g["penalties"], 5, 1, 1, np.uint32, devices=devs)
         for ps in g["passes"]:
             a_i = g["alphas"].index(ps["alpha"])
             p_i = g["penalties"].index(ps["penalty"])
             assert bits_equal(res["test"][0, a_i, p_i], np.array(ps["root_test"], np.float32)), devs
             assert bits_equal(res["train"][0, a_i, p_i], np.array(ps["root_train"], np.float32)), devs
-    monkeypatch.setenv("KMERPAPA_DEVICES", "0,0")
+            if len(devs) == 8:
+                ref = O.cv_pass(gp, contexts, Mf, Uf, ps["alpha"], res["betas"][0, a_i], ps["penalty"], 32)
+                assert bits_equal(res["train"][0, a_i, p_i], ref["root_train"]), devs
+                assert bits_equal(res["test"][0, a_i, p_i], ref["root_test"]), devs
+    monkeypatch.setenv("KMERPAPA_DEVICES", ",".join(["0"] * 8))
     buf = io.StringIO()
 
     class A:

@@ -307,3 +307,36 @@ def test_engine_run_groups_gpu_named_twice(monkeypatch):
         assert np.array_equal(rt, want)
         assert sorted(made) == sorted(zip(devs, engine._replicas(devs)))
     assert engine._replicas([1, 0, 1, 1]) == [0, 0, 1, 2]
+
+
+def test_cv_driver_over_8_devices_with_emulator_plans(monkeypatch):
+    """The CV driver's default runner (engine.run_groups with the pipelined fold feed) over 8
+    distinct device ids, each slot's plan an emulator-backed stand-in of engine.Plan
+    (tests/emu EmuPlan: counts_begin / counts_fold / run): the real lane-granular split,
+    fold pieces, pass packing, feeder threads and lane re-ordering run 8 wide, and the
+    roots and betas equal the single-process emulator run's bytes for a 5 x 5 grid."""
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.algorithms import bottum_up_array_penalty_plus_pseudo_CV as cvm
+    from tests.emu import emu as E
+    c = golden_json("small_dp.json")["cases"]["k3"]
+    ctx = {k: tuple(v) for k, v in c["contextD"].items()}
+    alphas, pens, nf = [0.5, 1.0, 2.0, 5.0, 10.0], [1.0, 2.0, 3.0, 4.0, 5.0], 5
+    plans = {}
+
+    def get_plan(dev, gp, mb=0, replica=0):
+        if (dev, replica) not in plans:
+            plans[(dev, replica)] = E.EmuPlan(gp, mb)
+        return plans[(dev, replica)]
+    monkeypatch.setattr(engine, "get_plan", get_plan)
+    ref = cvm.cv_roots(c["gen_pat"], ctx, alphas, pens, nf, 3, 1, np.uint32, run_groups=E.run_groups)
+    devs = list(range(8))
+    res = cvm.cv_roots(c["gen_pat"], ctx, alphas, pens, nf, 3, 1, np.uint32, devices=devs)
+    for key in ("train", "test", "betas"):
+        assert res[key].tobytes() == ref[key].tobytes(), key
+    assert sorted(d for d, _ in plans) == devs
+    lanes = {d: sum(n for p in plans[(d, 0)].passes for _, _, n in p) for d in devs}
+    assert sum(lanes.values()) == 125 and max(lanes.values()) - min(lanes.values()) <= 1
+    for d in devs:  # a share's passes run in fold order, each within the slot's reservation
+        folds = [max(f for f, _, _ in p) for p in plans[(d, 0)].passes]
+        assert folds == sorted(folds)
+        assert all(sum(n for _, _, n in p) <= plans[(d, 0)].reserved for p in plans[(d, 0)].passes)
