@@ -28,10 +28,13 @@ def _seq_sum_rows(terms):
     return s
 
 
-def allkmers_sums(M, U, alphas, betas):
+def allkmers_sums(M, U, alphas, betas, per_row=False):
     """``(sum_train, sum_test)`` ``[na, nf]`` for fold counts ``M``/``U`` ``[n, nf]``
     (uint64, matches() order) and ``betas`` ``[na, nf]`` -- the quantities kp_allkmers_cv
-    returns."""
+    returns.  ``per_row=True`` evaluates test_folds one k-mer row ([nf] arrays) at a time
+    as the reference's loop does (:38-44): numpy's vectorised division over a whole
+    [n, nf] table returns 0/0 as a NaN of the other sign than its [nf]-row path and the C
+    library (measured), so NaN encodings are compared per row; the values are the same."""
     M = np.asarray(M, np.uint64)
     U = np.asarray(U, np.uint64)
     trM = M.sum(axis=1, keepdims=True) - M
@@ -39,6 +42,14 @@ def allkmers_sums(M, U, alphas, betas):
     tr, te = [], []
     with np.errstate(divide="ignore", invalid="ignore"):
         for a, b in zip(alphas, np.asarray(betas, np.float64)):
+            if per_row:
+                s_tr, s_te = np.zeros(M.shape[1]), np.zeros(M.shape[1])
+                for i in range(M.shape[0]):
+                    s_tr += test_folds(trM[i], trU[i], trM[i], trU[i], a, b)
+                    s_te += test_folds(trM[i], trU[i], M[i], U[i], a, b)
+                tr.append(s_tr)
+                te.append(s_te)
+                continue
             tr.append(_seq_sum_rows(test_folds(trM, trU, trM, trU, a, b)))
             te.append(_seq_sum_rows(test_folds(trM, trU, M, U, a, b)))
     return np.array(tr).reshape(len(alphas), M.shape[1]), np.array(te).reshape(len(alphas), M.shape[1])

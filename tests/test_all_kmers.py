@@ -7,7 +7,8 @@ make_golden.py job allk5), digit for digit.
 GPU: the product path (kp_allkmers_cv, csrc/kp_allk.h) -- the CLI's output table and
 stderr byte-identical to those runs, and the float64 loss sums bit-identical to the
 oracle on the 9-mer benchmark counts (131,072 k-mers) and on edge cases (alpha = 0 with
-empty k-mers: 0/0 rates, NaN sums)."""
+empty k-mers: 0/0 rates, NaN sums, compared with the oracle's per-row evaluation as the
+reference's loop runs it)."""
 import numpy as np
 import pytest
 
@@ -127,7 +128,7 @@ def test_all_kmers_gpu_edge_cases_vs_oracle():
     betas = np.array([[0.0, 0.0, 0.0], [1e4, 2e4, 3e4], [5e5, 6e5, 7e5]])
     dev = engine.get_device(engine.visible_devices()[0])
     tr, te = dev.allkmers_cv(M, U, alphas, betas)
-    otr, ote = OA.allkmers_sums(M, U, alphas, betas)
+    otr, ote = OA.allkmers_sums(M, U, alphas, betas, per_row=True)  # the reference's per-k-mer rows
     assert np.isnan(tr[0]).any()
     assert np.array_equal(_bits(tr), _bits(otr)) and np.array_equal(_bits(te), _bits(ote))
     e_tr, e_te = dev.allkmers_cv(np.zeros((0, nf), np.uint64), np.zeros((0, nf), np.uint64), alphas, betas)
