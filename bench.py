@@ -279,7 +279,11 @@ def cv_run(plan, prep, gen_pat, groups):
     return {"wall_s": wall, "plan_tables_s": box["t_tables"], "fold_ready_s": [round(x, 4) for x in fold_t],
             "fold_split_s": fold_t[-1], "passes_start_s": t_start, "lanes": sum(len(g[3]) for g in groups),
             # per pass: lanes, [counts wait + upload, start, end] in s from the job's start
-            "passes": [[n, round(w, 4), round(a - t0, 4), round(b - t0, 4)] for _, n, w, a, b in log]}
+            "passes": [[n, round(w, 4), round(a - t0, 4), round(b - t0, 4)] for _, n, w, a, b, _ in log],
+            # the sweep kernels' HIP-event time and compulsory bytes over the share's passes
+            "kernel_ms": sum(st.get("dp_ms", 0.0) for *_, st in log),
+            "compulsory_bytes": sum(st.get("gather_bytes", 0.0) for *_, st in log),
+            "units": sum(st.get("units", 0) for *_, st in log)}
 
 
 def shadow_host_side(prep, gen_pat):
@@ -369,8 +373,16 @@ def model_world(plan, prep, gen_pat, world, shadows):
         shares.append(cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], r, world)))
         shadow_s += shadows.wait(world - 1)
         note(f"model {world} GPUs: share {r} {shares[-1]['wall_s']:.2f} s")
+    alloc = [prep["alloc_s_per_lane"] * max([n for n, *_ in x["passes"]] or [0]) for x in shares]
+    fracs = [x["compulsory_bytes"] / (x["kernel_ms"] / 1e3) / 1e9 / PEAK_HBM_GBS for x in shares if x["kernel_ms"]]
     return {"world": world, "share_s": [round(x["wall_s"], 4) for x in shares],
             "share_lanes": [x["lanes"] for x in shares],
+            # each rank allocates its widest pass's lanes once, in parallel with the others
+            "share_hbm_alloc_s": [round(a, 4) for a in alloc],
+            "wall_s_incl_alloc": max(x["wall_s"] + a for x, a in zip(shares, alloc)),
+            "units": sum(x["units"] for x in shares),
+            "share_kernel_ms": [round(x["kernel_ms"], 2) for x in shares],
+            "share_roofline_frac": [round(f, 4) for f in fracs],
             "share_passes_start_s": [round(x["passes_start_s"], 4) for x in shares],
             "share_fold_split_s": [round(x["fold_split_s"], 4) for x in shares],
             "share_fold0_s": [x["fold_ready_s"][0] for x in shares],
@@ -382,15 +394,17 @@ def model_world(plan, prep, gen_pat, world, shadows):
 def full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds=(2, 4, 8)):
     """The whole grid x folds as the CV driver runs it (cv_run: pipelined fold split,
     this rank's lane-granular share of the passes in fold order, root read-out) on the plan
-    the timed steps used.  The one-time HBM allocation is not in the wall-clock
-    (``prep["t_alloc"]``, reported beside it: on this platform it is dominated by the
-    driver wiping HBM that earlier processes freed, 0.05-6 s for 150 GB).  At world 1 it
-    also models the wall-clock of a job on 2, 4 and 8 GPUs (model_world)."""
+    the timed steps used.  The one-time HBM allocation of the lane buffers happened before
+    (the run's widest pass); ``wall_s`` excludes it and ``wall_s_incl_alloc`` adds this
+    rank's share of it (measured seconds per lane x the lanes of its widest pass: on this
+    platform dominated by the driver wiping HBM that earlier processes freed).  At world 1
+    it also models the wall-clock of a job on 2, 4 and 8 GPUs (model_world), each rank
+    paying its own allocation in parallel."""
     from kmerpapa_amd.shard import rank_groups
     out = cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], rank, world))
     note(f"full CV (rank {rank} of {world}) {out['wall_s']:.2f} s")
-    out["hbm_alloc_s"] = prep["t_alloc"]
-    out["wall_s_incl_alloc"] = out["wall_s"] + prep["t_alloc"]
+    out["hbm_alloc_s"] = prep["alloc_s_per_lane"] * max([n for n, *_ in out["passes"]] or [0])
+    out["wall_s_incl_alloc"] = out["wall_s"] + out["hbm_alloc_s"]
     if world == 1 and model_worlds:
         out["models"] = {}
         shadows = Shadows(max(model_worlds) - 1, prep["config"], gen_pat)
@@ -398,9 +412,35 @@ def full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds=(2, 4, 8)):
             for w in model_worlds:
                 m = model_world(plan, prep, gen_pat, w, shadows)
                 m["speedup"] = out["wall_s"] / m["wall_s"]
+                m["speedup_incl_alloc"] = out["wall_s_incl_alloc"] / m["wall_s_incl_alloc"]
                 out["models"][str(w)] = m
         finally:
             shadows.close()
+    return out
+
+
+def scaling_table(line, cv, prep, npat):
+    """patterns scored/s, kernel roofline fraction and CV wall-clock (with and without the
+    one-time lane allocation) at every GPU count north_star names: N = 1 measured (the
+    line's own step rate and roofline, the full CV run), N = 2, 4, 8 modelled (model_world:
+    every rank's share run on this GPU beside N - 1 concurrent host sides).  units_per_s =
+    the whole grid's units (cells x folds x (alpha, c)) / CV wall-clock; roofline_frac = the
+    sweep kernels' compulsory bytes / their HIP-event time / 8 TB/s, per GPU (min and mean
+    over the ranks); weak_units_per_s = N x the measured per-GPU step rate (what the
+    driver's scaling run measures)."""
+    total = npat * sum(len(g[3]) for g in prep["groups"])
+    out = {"1": {"units_per_s": total / cv["wall_s"], "units_per_s_incl_alloc": total / cv["wall_s_incl_alloc"],
+                 "roofline_frac": line["roofline"]["frac"], "roofline_frac_min": line["roofline"]["frac"],
+                 "wall_s": cv["wall_s"], "wall_s_incl_alloc": cv["wall_s_incl_alloc"],
+                 "hbm_alloc_s": cv["hbm_alloc_s"], "weak_units_per_s": line["value"], "measured": True}}
+    for w, m in (cv.get("models") or {}).items():
+        fr = m["share_roofline_frac"]
+        out[w] = {"units_per_s": total / m["wall_s"], "units_per_s_incl_alloc": total / m["wall_s_incl_alloc"],
+                  "roofline_frac": sum(fr) / len(fr) if fr else None, "roofline_frac_min": min(fr) if fr else None,
+                  "wall_s": m["wall_s"], "wall_s_incl_alloc": m["wall_s_incl_alloc"],
+                  "hbm_alloc_s": max(m["share_hbm_alloc_s"]), "speedup": m["speedup"],
+                  "speedup_incl_alloc": m["speedup_incl_alloc"], "weak_units_per_s": int(w) * line["value"],
+                  "measured": False}
     return out
 
 
@@ -455,8 +495,8 @@ def main():
     t0 = time.perf_counter()
     plan = engine.get_plan(prep["device"], gen_pat, a.max_block)
     prep["t_plan"] = time.perf_counter() - t0
-    cap = engine.pass_cap(groups, plan.lanes_that_fit())
     width = plan.info["lanes_per_workgroup"]
+    cap = engine.pass_cap(groups, plan.lanes_that_fit(), width)
     # a step = one pass of the whole grid's CV plan on one GPU (engine.plan_passes: fold
     # pieces of one workgroup's lanes; 9-mer: one (alpha, fold) group of 5 penalties; 11-mer:
     # 5 of a fold's 49 (alpha, c) lanes, some spanning two alphas)
@@ -466,8 +506,10 @@ def main():
     most = max([sum(len(g[3]) for g in p) for p in step_passes] +
                [sum(len(g[3]) for g in p) for w in worlds for passes in cv_shares(prep, w, cap, width) for p in passes])
     t0 = time.perf_counter()
-    plan.reserve(most)  # the one large allocation of the run (lane buffers, first-touched)
+    plan.reserve(most)  # the one large allocation of the run: the widest pass any modelled rank runs
     prep["t_alloc"] = time.perf_counter() - t0
+    prep["alloc_lanes"] = most
+    prep["alloc_s_per_lane"] = prep["t_alloc"] / most
     plan.set_counts(prep["Mk"], prep["Uk"])
 
     def step(s):
@@ -562,6 +604,10 @@ def main():
 
             "kernel_tag": tag,
         }
+        if cv:
+            line["scaling_by_gpus"] = scaling_table(line, cv, prep, plan.info["npat"])
+            line["hbm_alloc"] = {"lanes": prep["alloc_lanes"], "s": prep["t_alloc"],
+                                 "bytes": prep["alloc_lanes"] * plan.info["bytes_per_lane"]}
         if cv and "models" in cv:
             line["cv_full_grid_wall_s_model"] = {w: m["wall_s"] for w, m in cv["models"].items()}
             line["cv_full_grid_speedup_model"] = {w: m["speedup"] for w, m in cv["models"].items()}

@@ -72,8 +72,9 @@ typedef struct {
     double pairs_high;    /* ... of which at high (gathered) positions             */
     uint64_t bytes_per_lane; /* device bytes per lane: f32 train score per cell
                                 (value-only sweep) + backtrack node pool + leaves */
-    uint32_t lanes_per_workgroup; /* lanes one sweep workgroup holds (32-bit counts):
-                                     passes cut into pieces of this width run best */
+    uint32_t lanes_per_workgroup; /* lanes one sweep workgroup holds at the plan's count
+                                     width (32-bit until counts are set): passes cut
+                                     into pieces of this width run best */
     uint32_t pad_;
 } kp_plan_info;
 

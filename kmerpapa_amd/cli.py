@@ -122,7 +122,17 @@ def write_partition(out, names, counts, contextD, alpha, beta, long_output):
         from .engine import format_long_rows
         from .io_utils import KmerCounts
         rows = KmerCounts(contextD.k, codes, contextD.M[idx], contextD.U[idx])
-        text = format_long_rows(rows.letters(), rows.U, rows.M, pid, tails)
+        try:
+            text = format_long_rows(rows.letters(), rows.U, rows.M, pid, tails)
+        except ZeroDivisionError:
+            # a k-mer without counts: the reference prints every row before it and then
+            # raises (c_rate = c_pos / 0); write those rows the same way, then raise
+            letters = rows.letters()
+            for i in range(len(pid)):
+                cn, cp = int(rows.U[i]), int(rows.M[i])
+                ctx = letters[i].tobytes().decode("ascii")
+                out.write(f"{ctx} {cn} {cp} {cp / (cp + cn)}{tails[int(pid[i])]}")
+            raise
         out.flush()
         if hasattr(out, "buffer"):
             out.buffer.write(text)

@@ -607,7 +607,9 @@ void kp_plan_destroy(kp_plan *p) {
 
 static int wg_lanes(const kp::host_plan &hp, size_t ct_bytes, size_t lds_max);  // defined with the launch code
 
-static void info_of(const kp::host_plan &h, kp_plan_info *o) {
+// ct_bytes / lds_max: the count width and LDS of the plan's device once counts are set
+// (lanes_per_workgroup is then what kp_pass uses); 4 bytes and 160 KiB before that
+static void info_of(const kp::host_plan &h, kp_plan_info *o, size_t ct_bytes = 4, size_t lds_max = 160u * 1024u) {
     o->npat = h.npat;
     o->nblocks = h.g.nblocks;
     o->n_kmers = h.n_kmers;
@@ -622,13 +624,13 @@ static void info_of(const kp::host_plan &h, kp_plan_info *o) {
     // train scores + backtrack node pool + leaf list
     o->bytes_per_lane = h.g.nblocks * (uint64_t)h.g.Bpad * 4 + (uint64_t)node_cap_of(h) * sizeof(kp_node) +
                         h.n_kmers * 8 + 4096;
-    o->lanes_per_workgroup = (uint32_t)wg_lanes(h, 4, 160u * 1024u);
+    o->lanes_per_workgroup = (uint32_t)wg_lanes(h, ct_bytes, lds_max);
     o->pad_ = 0;
 }
 
 int kp_plan_get_info(const kp_plan *p, kp_plan_info *o) {
     if (!p || !o) return fail(KP_E_ARG, "null argument");
-    info_of(p->hp, o);
+    info_of(p->hp, o, p->ct_bytes ? (size_t)p->ct_bytes : 4u, p->ctx ? p->ctx->lds_max : 160u * 1024u);
     return KP_OK;
 }
 

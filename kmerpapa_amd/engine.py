@@ -175,6 +175,9 @@ def kernel_tag():
     files += [os.path.join(csrc, "gen_logdata.py"), os.path.join(csrc, "Makefile"),
               os.path.join(os.path.dirname(_HERE), "include", "kmerpapa_hip.h")]
     for fn in files:
+        if not os.path.isfile(fn):  # (an installed copy may lack a build file: hash its absence)
+            h.update(b"missing:" + os.path.basename(fn).encode())
+            continue
         with open(fn, "rb") as f:
             h.update(os.path.basename(fn).encode() + b"\0" + f.read())
     gen = os.path.join(csrc, "kp_logdata.h")
@@ -430,6 +433,14 @@ class Plan:
                                     int(M.dtype.itemsize)))
         self.nf = M.shape[1]
         self.itype = M.dtype
+        self._refresh_info()
+
+    def _refresh_info(self):
+        """Re-read the plan's info: lanes_per_workgroup depends on the count width, fixed
+        once counts are set (64-bit counts above 2^32 - 1 take more LDS)."""
+        info = KPPlanInfo()
+        _check(load().kp_plan_get_info(self._h, ctypes.byref(info)))
+        self.info = {name: getattr(info, name) for name, _ in KPPlanInfo._fields_}
 
     def counts_begin(self, M_all, U_all, nf):
         """Start a fold-by-fold count upload: ``M_all``/``U_all`` ``[n_kmers]`` = counts of
@@ -442,6 +453,7 @@ class Plan:
                                       int(M_all.dtype.itemsize)))
         self.nf = int(nf)
         self.itype = M_all.dtype
+        self._refresh_info()
 
     def counts_fold(self, fold, M_fold, U_fold):
         """Counts of one fold ``[n_kmers]`` (same itype as counts_begin; kp_counts_fold)."""
@@ -620,18 +632,24 @@ def materialize(M, U, groups):
     return M, U, groups
 
 
-# lanes a pass may hold when it packs groups of different widths (KMERPAPA_PASS_LANES)
-PASS_LANES = int(os.environ.get("KMERPAPA_PASS_LANES", "7"))
+# lanes a pass may hold when it packs groups of different widths (KMERPAPA_PASS_LANES; 0 =
+# one sweep workgroup's width, Plan.info["lanes_per_workgroup"])
+PASS_LANES = int(os.environ.get("KMERPAPA_PASS_LANES", "0"))
 
 
-def pass_cap(groups, fit):
-    """Lanes per pass: up to PASS_LANES (7), or the largest group if wider, if that fits.
-    A small group packed beside a full one costs less than alone (one pass's fixed work:
-    9-mer passes of 4+2 lanes 532-536 ms against 339 + 222 in two passes, 5+1 531 against
-    394 + 144); two 5-lane groups (10 lanes) never share a pass: passes of equal full groups
-    are not faster per lane and would need more HBM."""
+def pass_cap(groups, fit, width=0):
+    """Lanes per pass: PASS_LANES, by default one workgroup's ``width`` (5 at 9-mers), or
+    the largest group if wider, if that fits.  Packing a small piece beside a full one
+    saves one pass's fixed work (9-mer 5+1 lanes: 504 ms against 380 + 134), but every
+    lane of the widest pass is allocated for the whole job (30.8 GB per lane at 9-mers) and
+    a hipMalloc of HBM a process used before waits for the driver's wipe: 6.6-18 ms per GB
+    measured on the GPU box after the test suite (0.2-0.55 s per extra lane; fresh HBM 0.5
+    ms per GB, 15 ms per lane), more than the 10 ms the packing saves, so passes stay one
+    workgroup wide.  Two 5-lane groups never share a pass either: they are not
+    faster per lane."""
     widest = max([len(g[3]) for g in groups] or [1])
-    return min(fit, max(PASS_LANES, widest))
+    cap = PASS_LANES or width or 7
+    return min(fit, max(cap, widest))
 
 
 def pack_passes(groups, max_lanes):
@@ -810,7 +828,8 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0):
     def prep(dev, rep, chunk):
         if chunk:
             plan = get_plan(dev, gen_pat, max_block, replica=rep)
-            passes, _ = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()), plan.info["lanes_per_workgroup"])
+            width = plan.info["lanes_per_workgroup"]
+            passes, _ = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit(), width), width)
             plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
     threads = [threading.Thread(target=prep, args=(dev, rep, chunk))
                for dev, rep, chunk in zip(devices, _replicas(devices), _device_shares(groups, devices))]
@@ -856,8 +875,8 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
                 else:
                     plan.set_counts(M, U)
                 # passes in fold order (folds arrive in order), small groups beside a full one
-                passes, order = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit()),
-                                            plan.info["lanes_per_workgroup"])
+                width = plan.info["lanes_per_workgroup"]
+                passes, order = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit(), width), width)
                 plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))  # one allocation
                 outs = []
                 queued = {}
@@ -892,9 +911,9 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
                                 raise fed_err[0]
                         t_run = time.perf_counter()
                         outs.append(plan.run(pas))
-                        if PASS_LOG is not None:  # (slot, lanes, counts wait s, pass start, pass end)
+                        if PASS_LOG is not None:  # (slot, lanes, counts wait s, pass start, pass end, stats)
                             PASS_LOG.append((slot, sum(len(g[3]) for g in pas), t_run - t_wait, t_run,
-                                             time.perf_counter()))
+                                             time.perf_counter(), plan.stats() if hasattr(plan, "stats") else {}))
                 finally:
                     if feed is not None:
                         fth.join()

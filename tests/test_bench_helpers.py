@@ -38,15 +38,23 @@ def test_cv_shares_cover_every_lane_once():
         assert max(lanes) - min(lanes) <= 1
 
 
-def test_pass_cap_packs_small_groups_beside_full_ones():
+def test_pass_cap_is_one_workgroup_wide_by_default():
+    """Passes hold one workgroup's lanes (the job allocates its widest pass's lanes, and
+    HBM a process used before is wiped on allocation: an extra lane costs more than the
+    packing saves); a wider user group keeps its width; KMERPAPA_PASS_LANES
+    overrides."""
     groups = [(0, 1.0, 1.0, [1.0] * 5), (1, 1.0, 1.0, [1.0] * 3)]
-    assert engine.pass_cap(groups, 9) == engine.PASS_LANES == 7
-    assert engine.pass_cap(groups, 4) == 4
-    assert engine.pass_cap([(0, 1.0, 1.0, [1.0] * 8)], 9) == 8
-    assert engine.pass_cap([], 9) == min(9, engine.PASS_LANES)
-    # an 8-rank share of the 5x5x5 grid: [5, 5, 5, 1] -> passes [5], [5], [5, 1]
+    assert engine.PASS_LANES == 0
+    assert engine.pass_cap(groups, 9, 5) == 5
+    assert engine.pass_cap(groups, 9) == 7  # (no width known: the old 7-lane packing)
+    assert engine.pass_cap(groups, 4, 5) == 4
+    assert engine.pass_cap([(0, 1.0, 1.0, [1.0] * 8)], 9, 5) == 8
+    # an 8-rank share of the 5x5x5 grid: [5, 5, 5, 1] -> passes [5], [5], [5], [1]
     share = [(f, 1.0, 1.0, [1.0] * n) for f, n in enumerate([5, 5, 5, 1])]
-    assert [[len(g[3]) for g in p] for p in engine.pack_passes(share, engine.pass_cap(share, 9))] == [[5], [5], [5, 1]]
+    assert [[len(g[3]) for g in p] for p in engine.pack_passes(share, engine.pass_cap(share, 9, 5))] == \
+        [[5], [5], [5], [1]]
+    assert [[len(g[3]) for g in p] for p in engine.pack_passes(share, engine.pass_cap(share, 9))] == \
+        [[5], [5], [5, 1]]
 
 
 def test_plan_passes_fold_order_and_lane_mapping():

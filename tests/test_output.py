@@ -71,6 +71,11 @@ def test_long_output_zero_counts_raise_like_reference():
     from kmerpapa_amd.io_utils import KmerCounts
     codes = np.array([0, 1, 2, 3], np.uint64)
     table = KmerCounts(1, codes, [1, 0, 2, 3], [5, 0, 7, 9])
+    buf = io.StringIO()
     with pytest.raises(ZeroDivisionError):
-        write_partition(io.StringIO(), ["N"], [(6, 21)], table, 0.5, 1.0, True)
+        write_partition(buf, ["N"], [(6, 21)], table, 0.5, 1.0, True)
+    # the reference prints every row before the k-mer without counts, then raises
+    lines = buf.getvalue().splitlines()
+    assert lines == ["context c_neg c_pos c_rate pattern p_neg p_pos p_rate",
+                     f"A 5 1 {1 / 6} N 21 6 {(6 + 0.5) / (6 + 21 + 0.5 + 1.0)}"]
     assert list(itertools.islice(engine.py_repr([0.25]), 1)) == ["0.25"]
