@@ -373,11 +373,13 @@ def model_world(plan, prep, gen_pat, world, shadows):
         shares.append(cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], r, world)))
         shadow_s += shadows.wait(world - 1)
         note(f"model {world} GPUs: share {r} {shares[-1]['wall_s']:.2f} s")
-    alloc = [prep["alloc_s_per_lane"] * max([n for n, *_ in x["passes"]] or [0]) for x in shares]
+    alloc = [prep["t_alloc"] for _ in shares]  # every rank's GPU in the state this one was in
     fracs = [x["compulsory_bytes"] / (x["kernel_ms"] / 1e3) / 1e9 / PEAK_HBM_GBS for x in shares if x["kernel_ms"]]
     return {"world": world, "share_s": [round(x["wall_s"], 4) for x in shares],
             "share_lanes": [x["lanes"] for x in shares],
-            # each rank allocates its widest pass's lanes once, in parallel with the others
+            # each rank allocates its lane buffers once, in parallel with the others, and waits
+            # as long as this run's allocation did (the wait is the driver finishing its wipe of
+            # HBM earlier processes freed, not a cost per byte allocated: DESIGN.md 2)
             "share_hbm_alloc_s": [round(a, 4) for a in alloc],
             "wall_s_incl_alloc": max(x["wall_s"] + a for x, a in zip(shares, alloc)),
             "units": sum(x["units"] for x in shares),
@@ -395,15 +397,16 @@ def full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds=(2, 4, 8)):
     """The whole grid x folds as the CV driver runs it (cv_run: pipelined fold split,
     this rank's lane-granular share of the passes in fold order, root read-out) on the plan
     the timed steps used.  The one-time HBM allocation of the lane buffers happened before
-    (the run's widest pass); ``wall_s`` excludes it and ``wall_s_incl_alloc`` adds this
-    rank's share of it (measured seconds per lane x the lanes of its widest pass: on this
-    platform dominated by the driver wiping HBM that earlier processes freed).  At world 1
-    it also models the wall-clock of a job on 2, 4 and 8 GPUs (model_world), each rank
-    paying its own allocation in parallel."""
+    (the run's widest pass); ``wall_s`` excludes it and ``wall_s_incl_alloc`` adds it as
+    measured.  On this platform that time is a wait for the driver to finish wiping HBM
+    that earlier processes freed (~36 GB/s of freed bytes, whatever the request's size;
+    1 ms for 150 GB on a GPU idle for a few seconds: tools/alloc_seq.sh).  At
+    world 1 it also models the wall-clock of a job on 2, 4 and 8 GPUs (model_world), each
+    rank waiting as long in parallel."""
     from kmerpapa_amd.shard import rank_groups
     out = cv_run(plan, prep, gen_pat, rank_groups(prep["groups"], rank, world))
     note(f"full CV (rank {rank} of {world}) {out['wall_s']:.2f} s")
-    out["hbm_alloc_s"] = prep["alloc_s_per_lane"] * max([n for n, *_ in out["passes"]] or [0])
+    out["hbm_alloc_s"] = prep["t_alloc"]
     out["wall_s_incl_alloc"] = out["wall_s"] + out["hbm_alloc_s"]
     if world == 1 and model_worlds:
         out["models"] = {}
@@ -509,7 +512,6 @@ def main():
     plan.reserve(most)  # the one large allocation of the run: the widest pass any modelled rank runs
     prep["t_alloc"] = time.perf_counter() - t0
     prep["alloc_lanes"] = most
-    prep["alloc_s_per_lane"] = prep["t_alloc"] / most
     plan.set_counts(prep["Mk"], prep["Uk"])
 
     def step(s):

@@ -641,12 +641,13 @@ def pass_cap(groups, fit, width=0):
     """Lanes per pass: PASS_LANES, by default one workgroup's ``width`` (5 at 9-mers), or
     the largest group if wider, if that fits.  Packing a small piece beside a full one
     saves one pass's fixed work (9-mer 5+1 lanes: 504 ms against 380 + 134), but every
-    lane of the widest pass is allocated for the whole job (30.8 GB per lane at 9-mers) and
-    a hipMalloc of HBM a process used before waits for the driver's wipe: 6.6-18 ms per GB
-    measured on the GPU box after the test suite (0.2-0.55 s per extra lane; fresh HBM 0.5
-    ms per GB, 15 ms per lane), more than the 10 ms the packing saves, so passes stay one
-    workgroup wide.  Two 5-lane groups never share a pass either: they are not
-    faster per lane."""
+    lane of the widest pass is allocated for the whole job (30.8 GB per lane at 9-mers),
+    and an allocation that does not fit the HBM the driver has finished wiping waits for
+    the whole wipe of what earlier processes freed (~36 GB/s; 5.6 s after a 200 GB
+    process, tools/alloc_seq.sh): the smaller reservation is the likelier to fit, which is
+    worth more than the 10 ms the packing saves, so passes stay one workgroup wide
+    (DESIGN.md 6).  Two 5-lane groups never share a pass either: they are not faster per
+    lane."""
     widest = max([len(g[3]) for g in groups] or [1])
     cap = PASS_LANES or width or 7
     return min(fit, max(cap, widest))
