@@ -277,31 +277,6 @@ __host__ __device__ inline uint32_t kp_st_idx(uint32_t l, uint32_t j, uint32_t b
     return L2 * bp + l;
 }
 
-// Item `it` of a block's NL x (Bpad / 4) float4 items (4 consecutive cells of one lane) as
-// (lane, 4-cell chunk), plane by plane (kp_st_idx) with the plane's lanes fastest: the
-// threads of a wave then write (gather) and read (store) a plane's cells with its lanes
-// side by side, 4-way LDS bank conflicts instead of 16-way for a lane-major order, while
-// each lane row is still read from HBM in 256-byte runs.
-template <int NL>
-__host__ __device__ inline void kp_st_item(uint32_t it, uint32_t nch, uint32_t *ll, uint32_t *c) {
-    constexpr uint32_t Q4 = NL / 4, L2 = 4 * Q4 + ((NL % 4) >= 2 ? 2u : 0u);
-    const uint32_t lane_major = it / nch;  // (the plane holding item it: same lane bounds)
-    uint32_t s, w;
-    if (lane_major < 4 * Q4) {
-        s = lane_major & ~3u;
-        w = 4;
-    } else if (lane_major < L2) {
-        s = 4 * Q4;
-        w = 2;
-    } else {
-        s = lane_major;
-        w = 1;
-    }
-    const uint32_t local = it - s * nch;
-    *ll = s + local % w;
-    *c = local / w;
-}
-
 // min over NP split pairs of one low position for W lanes starting at lane j0 (LDS layout
 // kp_st_idx); all 2*NP*W LDS reads issue before the first min (fully unrolled)
 template <int NL, int W, int NP, typename SP>

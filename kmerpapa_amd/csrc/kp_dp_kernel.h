@@ -179,13 +179,12 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
     const uint32_t Bpad = g.Bpad, nch = Bpad / 4, nitems = (uint32_t)NL * nch;
     const float inf = __builtin_huge_valf();
     for (uint32_t it0 = threadIdx.x; it0 < nitems; it0 += NI * blockDim.x) {
-        uint32_t it[NI], o[NI], il[NI], ic[NI];
+        uint32_t it[NI], o[NI];
         float4 best[NI];
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             it[i] = (it0 + i * blockDim.x < nitems) ? it0 + i * blockDim.x : it0;
-            kp_st_item<NL>(it[i], nch, &il[i], &ic[i]);
-            o[i] = (lane0 + il[i]) * Bpad + 4 * ic[i];
+            o[i] = (lane0 + it[i] / nch) * Bpad + 4 * (it[i] % nch);
             best[i] = make_float4(inf, inf, inf, inf);
         }
         if (nnt > 0) kp_gather_range<NI, PU, true>(P, hp, 0, nnt, o, best);
@@ -193,7 +192,7 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             if (i > 0 && it[i] == it0) break;
-            const uint32_t ll = il[i], c = ic[i];
+            const uint32_t ll = it[i] / nch, c = it[i] % nch;
             if (4 * c + 4 > g.B) {
                 if (4 * c + 0 >= g.B) best[i].x = inf;
                 if (4 * c + 1 >= g.B) best[i].y = inf;
@@ -523,8 +522,7 @@ kp_dp_kernel(kp_dp_params P) {
     // ---- store the block's score rows ----
     const uint32_t nch = Bpad / 4;
     for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
-        uint32_t ll, c;
-        kp_st_item<NL>(item, nch, &ll, &c);
+        const uint32_t ll = item / nch, c = item % nch;
         float4 *dst = reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c);
         const float4 v = make_float4(st[kp_st_idx<NL>(4 * c + 0, ll, Bpad)], st[kp_st_idx<NL>(4 * c + 1, ll, Bpad)],
                                      st[kp_st_idx<NL>(4 * c + 2, ll, Bpad)], st[kp_st_idx<NL>(4 * c + 3, ll, Bpad)]);
