@@ -115,14 +115,6 @@ __device__ inline uint64_t kp_rfl64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-// component k (0..3, per thread) of a float4 / of a 4-float register array, as selects
-__device__ inline float kp_pick4(const float4 v, uint32_t k) {
-    return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-}
-__device__ inline float kp_pick_r4(const float (&r)[4], uint32_t k) {
-    return k == 0 ? r[0] : k == 1 ? r[1] : k == 2 ? r[2] : r[3];
-}
-
 // float4 min-update with a split candidate a + b (fminf drops NaN candidates like "<")
 __device__ inline void kp_min4v(float4 &best, const float4 a, const float4 b) {
     best.x = fminf(best.x, a.x + b.x);
@@ -207,13 +199,10 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
                 if (4 * c + 2 >= g.B) best[i].z = inf;
                 if (4 * c + 3 >= g.B) best[i].w = inf;
             }
-            // the 4 cells in a rotated order, so that the 4-lane plane's writes of a wave
-            // spread over 8 bank slots (4-way conflicts) instead of 2 (kp_st_idx)
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {
-                const uint32_t k = ((c >> 1) + q) & 3u;
-                st[kp_st_idx<NL>(4 * c + k, ll, Bpad)] = kp_pick4(best[i], k);
-            }
+            st[kp_st_idx<NL>(4 * c + 0, ll, Bpad)] = best[i].x;
+            st[kp_st_idx<NL>(4 * c + 1, ll, Bpad)] = best[i].y;
+            st[kp_st_idx<NL>(4 * c + 2, ll, Bpad)] = best[i].z;
+            st[kp_st_idx<NL>(4 * c + 3, ll, Bpad)] = best[i].w;
         }
     }
 }
@@ -535,12 +524,8 @@ kp_dp_kernel(kp_dp_params P) {
     for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
         const uint32_t ll = item / nch, c = item % nch;
         float4 *dst = reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c);
-        float r[4];  // (rotated order, as the gather writes them)
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) r[q] = st[kp_st_idx<NL>(4 * c + (((c >> 1) + q) & 3u), ll, Bpad)];
-        const uint32_t k0 = (4u - ((c >> 1) & 3u)) & 3u;  // r[q] holds cell (q + (c >> 1)) & 3: cell j is r[(j + k0) & 3]
-        const float4 v = make_float4(kp_pick_r4(r, k0), kp_pick_r4(r, (k0 + 1) & 3u), kp_pick_r4(r, (k0 + 2) & 3u),
-                                     kp_pick_r4(r, (k0 + 3) & 3u));
+        const float4 v = make_float4(st[kp_st_idx<NL>(4 * c + 0, ll, Bpad)], st[kp_st_idx<NL>(4 * c + 1, ll, Bpad)],
+                                     st[kp_st_idx<NL>(4 * c + 2, ll, Bpad)], st[kp_st_idx<NL>(4 * c + 3, ll, Bpad)]);
         if (P.ntstore) {
             typedef float kp_f4v __attribute__((ext_vector_type(4)));
             const kp_f4v w = {v.x, v.y, v.z, v.w};
