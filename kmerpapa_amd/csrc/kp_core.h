@@ -261,27 +261,10 @@ __host__ __device__ inline uint32_t kp_mul24(uint32_t a, uint32_t b) { return (a
 // fminf: it ignores NaN exactly as "v < best" does, and every score is >= +0 (no -0).
 // ---------------------------------------------------------------------------
 
-// LDS layout of a block's NL lanes (st): lane planes of 4, then 2, then 1 lanes, each
-// [bp][width] floats (bp = Bpad, a multiple of 16), in lane order -- 5 lanes = a 4-lane
-// plane + a 1-lane plane, 6 = 4 + 2, 7 = 4 + 2 + 1, 8 = 4 + 4.  A cell's lanes of one plane
-// are one aligned 16-, 8- or 4-byte word, so a split child's NL scores are one LDS read per
-// plane (5 lanes: a 16-byte and a 4-byte read; interleaved at stride 5 they took two
-// ds_read2_b32 and a ds_read_b32, whose 32-bank groups also conflict more).  1, 2 and 4
-// lanes keep the interleaved layout (one plane).
-template <int NL>
-__host__ __device__ inline uint32_t kp_st_idx(uint32_t l, uint32_t j, uint32_t bp) {
-    constexpr uint32_t Q4 = NL / 4, L2 = 4 * Q4 + ((NL % 4) >= 2 ? 2u : 0u);
-    bp &= ~15u;  // (Bpad is a multiple of 16: tells the compiler the planes are 64-byte aligned)
-    if (j < 4 * Q4) return (j >> 2) * 4u * bp + l * 4u + (j & 3u);
-    if (j < L2) return 4u * Q4 * bp + l * 2u + (j - 4u * Q4);
-    return L2 * bp + l;
-}
-
-// min over NP split pairs of one low position for W lanes starting at lane j0 (LDS layout
-// kp_st_idx); all 2*NP*W LDS reads issue before the first min (fully unrolled)
+// min over NP split pairs of one low position for W lanes starting at lane j0 (lane
+// stride NL); all 2*NP*W LDS reads issue before the first min (fully unrolled)
 template <int NL, int W, int NP, typename SP>
-__host__ __device__ inline void kp_pairs_minv(SP st, uint32_t bp, uint32_t l, uint32_t cg, uint64_t w, uint32_t j0,
-                                              float *lmin) {
+__host__ __device__ inline void kp_pairs_minv(SP st, uint32_t l, uint32_t cg, uint64_t w, uint32_t j0, float *lmin) {
     float va[NP][W], vb[NP][W];
     const uint32_t w0 = (uint32_t)w, w1 = (uint32_t)(w >> 32);
 #pragma unroll
@@ -291,8 +274,8 @@ __host__ __device__ inline void kp_pairs_minv(SP st, uint32_t bp, uint32_t l, ui
         const uint32_t l2 = l - kp_mul24((wp >> 4) & 15u, cg);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-            va[p][j] = st[kp_st_idx<NL>(l1, j0 + j, bp)];
-            vb[p][j] = st[kp_st_idx<NL>(l2, j0 + j, bp)];
+            va[p][j] = st[l1 * NL + j0 + j];
+            vb[p][j] = st[l2 * NL + j0 + j];
         }
     }
 #pragma unroll
@@ -331,9 +314,9 @@ __host__ __device__ inline bool kp_fast_logs_ok(const double *pen, int n, double
 
 // a cell's final score per lane: min(best split, single term).  MIX: lanes j0 + j >= sc.js
 // take the second (alpha, beta) set (sc.logp2 / sc.log1mp2; sc.a2 / sc.b2)
-template <int NL, int W, bool MIX = false, typename SP>
-__host__ __device__ inline void kp_cell_store(SP st, uint32_t bp, uint32_t l, const float *lmin, const kp_single_ctx &sc,
-                                              const double *pen, double alpha, double beta, uint32_t j0 = 0) {
+template <int W, bool MIX = false, typename SP>
+__host__ __device__ inline void kp_cell_store(SP row, const float *lmin, const kp_single_ctx &sc, const double *pen,
+                                              double alpha, double beta, uint32_t j0 = 0) {
     float out[W];
     bool unsafe = sc.exact;
     if (MIX) {  // one loop, each lane's term computed once (A/B: 1-2 ms faster per mixed pass)
@@ -377,11 +360,11 @@ __host__ __device__ inline void kp_cell_store(SP st, uint32_t bp, uint32_t l, co
         }
     }
 #pragma unroll
-    for (int j = 0; j < W; ++j) st[kp_st_idx<NL>(l, j0 + j, bp)] = out[j];
+    for (int j = 0; j < W; ++j) row[j] = out[j];
 }
 
-// one DP cell for lanes j0 .. j0+W-1 of the NL lanes in LDS (layout kp_st_idx, bp =
-// Bpad); the cell's slots hold the best high-position split gathered from HBM.
+// one DP cell for lanes j0 .. j0+W-1 of the NL lanes interleaved in LDS
+// (st[cell * NL + lane]); st[l] holds the best high-position split gathered from HBM.
 // pw = pair words [t][16]; pen = the W penalties of those lanes.  W = NL is the normal
 // mode (one thread per cell); W = 1 splits a cell's lanes over threads when a level has
 // few cells (shorter dependent chains on the narrow top levels of a block).
@@ -389,15 +372,15 @@ template <int NL, int W, typename SP, typename WP>
 __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint32_t l, uint32_t lowinfo, SP st,
                                                   const kp_single_ctx &sc, double alpha, double beta,
                                                   const double *pen, uint32_t j0 = 0) {
-    const uint32_t bp = g.Bpad;
+    SP row = st + l * NL + j0;
     if (__builtin_expect(sc.kmer, 0)) {  // level 0 (CV :145-151 / Fit :106-114)
 #pragma unroll
-        for (int j = 0; j < W; ++j) st[kp_st_idx<NL>(l, j0 + j, bp)] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
+        for (int j = 0; j < W; ++j) row[j] = kp_kmer_train(sc.c, alpha, beta, pen[j]);
         return;
     }
     float lmin[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) lmin[j] = st[kp_st_idx<NL>(l, j0 + j, bp)];
+    for (int j = 0; j < W; ++j) lmin[j] = row[j];
     uint64_t w[KP_MAXT];
 #pragma unroll
     for (int i = 0; i < KP_MAXT; ++i) w[i] = (i < g.t) ? pw[i * 16 + kp_low_digit(lowinfo, i)] : 0;
@@ -409,28 +392,28 @@ __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint3
         const uint32_t np = (uint32_t)(w[i] >> 56);
         const uint32_t cg = (uint32_t)g.cgl[i] & 0xFFFFu;  // low place values are < 2^16 (block <= 65535)
         if (np == 1) {
-            kp_pairs_minv<NL, W, 1>(st, bp, l, cg, w[i], j0, lmin);
+            kp_pairs_minv<NL, W, 1>(st, l, cg, w[i], j0, lmin);
         } else if (np == 3) {
-            kp_pairs_minv<NL, W, 3>(st, bp, l, cg, w[i], j0, lmin);
+            kp_pairs_minv<NL, W, 3>(st, l, cg, w[i], j0, lmin);
         } else if (np == 7) {
-            kp_pairs_minv<NL, W, 7>(st, bp, l, cg, w[i], j0, lmin);
+            kp_pairs_minv<NL, W, 7>(st, l, cg, w[i], j0, lmin);
         } else {
             for (uint32_t p = 0; p < np; ++p) {  // not produced by the IUPAC tables; kept general
                 const uint32_t l1 = l - (uint32_t)((w[i] >> (8 * p)) & 15u) * cg;
                 const uint32_t l2 = l - (uint32_t)((w[i] >> (8 * p + 4)) & 15u) * cg;
 #pragma unroll
                 for (int j = 0; j < W; ++j)
-                    lmin[j] = fminf(lmin[j], st[kp_st_idx<NL>(l1, j0 + j, bp)] + st[kp_st_idx<NL>(l2, j0 + j, bp)]);
+                    lmin[j] = fminf(lmin[j], st[l1 * NL + j0 + j] + st[l2 * NL + j0 + j]);
             }
         }
     }
-    kp_cell_store<NL, W>(st, bp, l, lmin, sc, pen, alpha, beta, j0);
+    kp_cell_store<W>(row, lmin, sc, pen, alpha, beta);
 }
 
 // min over one 4-pair chunk of a cell's split-pair list (c1 | c2 << 16 per pair, kp_plan.h
 // lpairs) for W lanes from j0; all 8*W LDS reads issue before the first min
 template <int NL, int W, int NPC = 4, typename SP>
-__host__ __device__ inline void kp_chunk_minv(SP st, uint32_t bp, const uint4 c, uint32_t j0, float *lmin) {
+__host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0, float *lmin) {
     const uint32_t e[4] = {c.x, c.y, c.z, c.w};
     float va[4][W], vb[4][W];
 #pragma unroll
@@ -438,8 +421,8 @@ __host__ __device__ inline void kp_chunk_minv(SP st, uint32_t bp, const uint4 c,
         const uint32_t c1 = e[p] & 0xFFFFu, c2 = e[p] >> 16;
 #pragma unroll
         for (int j = 0; j < W; ++j) {
-            va[p][j] = st[kp_st_idx<NL>(c1, j0 + j, bp)];
-            vb[p][j] = st[kp_st_idx<NL>(c2, j0 + j, bp)];
+            va[p][j] = st[c1 * NL + j0 + j];
+            vb[p][j] = st[c2 * NL + j0 + j];
         }
     }
 #pragma unroll
@@ -456,37 +439,38 @@ __host__ __device__ inline void kp_chunk_minv(SP st, uint32_t bp, const uint4 c,
 // longest list; shorter lists end in (B, B) pairs that read the +inf slot B.
 template <int NL, int W, bool MIX = false, int PRE = KP_PRE_CHUNKS, typename SP>
 __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, const uint4 *pre, const uint4 *lp, SP st,
-                                                uint32_t bp, const kp_single_ctx &sc, double alpha, double beta,
+                                                const kp_single_ctx &sc, double alpha, double beta,
                                                 const double *pen, uint32_t j0 = 0) {
+    SP row = st + l * NL + j0;
     if (__builtin_expect(sc.kmer, 0)) {  // level 0 (CV :145-151 / Fit :106-114)
 #pragma unroll
         for (int j = 0; j < W; ++j) {
             const bool s2 = MIX && (int)(j0 + j) >= sc.js;
-            st[kp_st_idx<NL>(l, j0 + j, bp)] = kp_kmer_train(sc.c, s2 ? sc.a2 : alpha, s2 ? sc.b2 : beta, pen[j]);
+            row[j] = kp_kmer_train(sc.c, s2 ? sc.a2 : alpha, s2 ? sc.b2 : beta, pen[j]);
         }
         return;
     }
     float lmin[W];
 #pragma unroll
-    for (int j = 0; j < W; ++j) lmin[j] = st[kp_st_idx<NL>(l, j0 + j, bp)];
+    for (int j = 0; j < W; ++j) lmin[j] = row[j];
 #ifdef KP_HALF_CHUNKS
     // a chunk whose last two pairs are padding runs as a 2-pair chunk
 #pragma unroll
     for (int k = 0; k < PRE; ++k)
         if (4u * k < npairs) {
             if (npairs - 4u * k > 2u)
-                kp_chunk_minv<NL, W>(st, bp, pre[k], j0, lmin);
+                kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
             else
-                kp_chunk_minv<NL, W, 2>(st, bp, pre[k], j0, lmin);
+                kp_chunk_minv<NL, W, 2>(st, pre[k], j0, lmin);
         }
-    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, bp, lp[k], j0, lmin);
+    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
 #else
 #pragma unroll
     for (int k = 0; k < PRE; ++k)
-        if (4u * k < npairs) kp_chunk_minv<NL, W>(st, bp, pre[k], j0, lmin);
-    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, bp, lp[k], j0, lmin);
+        if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
+    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
 #endif
-    kp_cell_store<NL, W, MIX>(st, bp, l, lmin, sc, pen, alpha, beta, j0);
+    kp_cell_store<W, MIX>(row, lmin, sc, pen, alpha, beta, j0);
 }
 
 // ---------------------------------------------------------------------------

@@ -199,10 +199,11 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
                 if (4 * c + 2 >= g.B) best[i].z = inf;
                 if (4 * c + 3 >= g.B) best[i].w = inf;
             }
-            st[kp_st_idx<NL>(4 * c + 0, ll, Bpad)] = best[i].x;
-            st[kp_st_idx<NL>(4 * c + 1, ll, Bpad)] = best[i].y;
-            st[kp_st_idx<NL>(4 * c + 2, ll, Bpad)] = best[i].z;
-            st[kp_st_idx<NL>(4 * c + 3, ll, Bpad)] = best[i].w;
+            float *sl = st + (size_t)(4 * c) * NL + ll;
+            sl[0] = best[i].x;
+            sl[NL] = best[i].y;
+            sl[2 * NL] = best[i].z;
+            sl[3 * NL] = best[i].w;
         }
     }
 }
@@ -257,7 +258,7 @@ kp_dp_kernel(kp_dp_params P) {
     const bool exact = P.exact != 0 || !kp_fast_logs_ok(G->pen, G->nl, alpha, beta) ||
                        (MIX && js < NL && !kp_fast_logs_ok(G->pen, G->nl, alpha2, beta2));
 
-    // LDS: st = NL lanes x Bpad f32 (lane planes, kp_st_idx) | ptab[PE][2] CT | hp[] | lm[t][16]
+    // LDS: st[Bpad][NL] f32 (lanes interleaved) | ptab[PE][2] CT | hp[] | lm[t][16]
     //      (count-table scratch aliases st, which the gather fills afterwards; every carve
     //       offset is a multiple of 16 bytes)
     const size_t st_bytes = (size_t)NL * Bpad * 4, scr_bytes = (size_t)P.pscratch_entries * 4 * sizeof(CT);
@@ -320,7 +321,6 @@ kp_dp_kernel(kp_dp_params P) {
     }
     for (uint32_t e = threadIdx.x; e < (uint32_t)g.t * 16u; e += blockDim.x) lm[e] = P.T.lowmask[e];
     __syncthreads();  // lm is read by every thread below
-    KP_STAMP(25);     // (stamps build: block setup -- high pairs, nucleotide masks -- apart from the count tables)
 
     // ---- separable count tables (train counts of the group fold), kp_core.h ----
     // (kp_kl_counts of the preloaded row: train = all data - fold, CV :22-24)
@@ -407,7 +407,7 @@ kp_dp_kernel(kp_dp_params P) {
                 const uint4 *lp = P.T.lpairs + (cur[0].w >> 8);
                 const uint32_t nch = (npairs + 3u) >> 2;
                 for (uint32_t c = (uint32_t)r; c < nch; c += KP_PS)
-                    kp_chunk_minv<NL, 1>((kp_lds_f32 *)st, Bpad, lp[c], j, &part);
+                    kp_chunk_minv<NL, 1>((kp_lds_f32 *)st, lp[c], j, &part);
 #pragma unroll
                 for (int m = 1; m < KP_PS; m <<= 1) part = fminf(part, __shfl_xor(part, m, KP_PS));
                 if (r == 0) {
@@ -423,13 +423,13 @@ kp_dp_kernel(kp_dp_params P) {
                         sc.logp = KP_DLOG(pr);
                         sc.log1mp = KP_DLOG(1.0 - pr);
                     }
-                    kp_lds_f32 *stl = (kp_lds_f32 *)st;
+                    kp_lds_f32 *row = (kp_lds_f32 *)st + l * NL + j;
                     const double pj = NL <= 2 ? kp_pick(pen, j) : G->pen[j];  // (registers: 2 lanes 185 -> 179 ms; 3-5 lanes slower)
                     if (sc.kmer) {
-                        stl[kp_st_idx<NL>(l, j, Bpad)] = kp_kmer_train(sc.c, aj, bj, pj);
+                        row[0] = kp_kmer_train(sc.c, aj, bj, pj);
                     } else {
-                        const float lmin = fminf(stl[kp_st_idx<NL>(l, j, Bpad)], part);
-                        kp_cell_store<NL, 1>(stl, Bpad, l, &lmin, sc, &pj, aj, bj, j);
+                        const float lmin = fminf(row[0], part);
+                        kp_cell_store<1>(row, &lmin, sc, &pj, aj, bj, j);
                     }
                 }
             }  // (act is uniform over a group's KP_PS lanes: a shuffle only reads active lanes)
@@ -462,8 +462,7 @@ kp_dp_kernel(kp_dp_params P) {
                     sc.log1mp = KP_DLOG(1.0 - pr);
                 }
                 const double pj = NL <= 2 ? kp_pick(pen, j) : G->pen[j];  // (registers: 2 lanes 185 -> 179 ms; 3-5 lanes slower)
-                kp_dp_cell_list<NL, 1, false, KP_NARROW_CHUNKS>(l, npairs, pre, lp, (kp_lds_f32 *)st, Bpad, sc, aj, bj,
-                                                                 &pj, j);
+                kp_dp_cell_list<NL, 1, false, KP_NARROW_CHUNKS>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, aj, bj, &pj, j);
             }
         } else
 #pragma unroll
@@ -505,11 +504,11 @@ kp_dp_kernel(kp_dp_params P) {
                     }
                 }
                 if (!KP_SKIP(P, 8)) {
-                    kp_dp_cell_list<NL, NL, MIX>(l, npairs, pre, lp, (kp_lds_f32 *)st, Bpad, sc, alpha, beta, pen);
+                    kp_dp_cell_list<NL, NL, MIX>(l, npairs, pre, lp, (kp_lds_f32 *)st, sc, alpha, beta, pen);
                 } else {  // timing ablation: no split scan, keep the single term
 #pragma unroll
                     for (int j = 0; j < NL; ++j)
-                        st[kp_st_idx<NL>(l, j, Bpad)] = (float)kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
+                        st[l * NL + j] = (float)kp_single_train(sc.c, sc.logp, sc.log1mp, pen[j]);
                 }
             }
         }
@@ -523,9 +522,9 @@ kp_dp_kernel(kp_dp_params P) {
     const uint32_t nch = Bpad / 4;
     for (uint32_t item = threadIdx.x; item < (uint32_t)NL * nch; item += blockDim.x) {
         const uint32_t ll = item / nch, c = item % nch;
+        const float *sl = st + (size_t)(4 * c) * NL + ll;
         float4 *dst = reinterpret_cast<float4 *>(P.S + h * rowstride + (uint64_t)(lane0 + ll) * Bpad + 4 * c);
-        const float4 v = make_float4(st[kp_st_idx<NL>(4 * c + 0, ll, Bpad)], st[kp_st_idx<NL>(4 * c + 1, ll, Bpad)],
-                                     st[kp_st_idx<NL>(4 * c + 2, ll, Bpad)], st[kp_st_idx<NL>(4 * c + 3, ll, Bpad)]);
+        const float4 v = make_float4(sl[0], sl[NL], sl[2 * NL], sl[3 * NL]);
         if (P.ntstore) {
             typedef float kp_f4v __attribute__((ext_vector_type(4)));
             const kp_f4v w = {v.x, v.y, v.z, v.w};

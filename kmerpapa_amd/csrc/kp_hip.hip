@@ -1308,8 +1308,8 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
     {
         unsigned long long hs[32];
         KP_HIP(hipMemcpy(hs, P.stamps, sizeof(hs), hipMemcpyDeviceToHost));
-        fprintf(stderr, "KP_STAMPS setup %.4g init %.4g gather %.4g store %.4g wg_ticks %.4g wg_real100MHz %.4g levels",
-                (double)hs[25], (double)hs[0], (double)hs[1], (double)hs[2], (double)hs[30], (double)hs[31]);
+        fprintf(stderr, "KP_STAMPS init %.4g gather %.4g store %.4g wg_ticks %.4g wg_real100MHz %.4g levels",
+                (double)hs[0], (double)hs[1], (double)hs[2], (double)hs[30], (double)hs[31]);
         for (int l = 0; l <= hp.lmax; ++l) fprintf(stderr, " %.4g", (double)hs[3 + l]);
         fprintf(stderr, "\n");
     }

@@ -19,31 +19,17 @@
 namespace {
 std::string g_err;
 
-// slot of (cell l, lane j) of an nl-lane block in LDS (the kernel's lane-plane layout)
-size_t st_idx(int nl, uint32_t l, uint32_t j, uint32_t bp) {
+void cell_values(int nl, uint32_t l, uint32_t npairs, const uint4 *lp, float *st, const kp_single_ctx &sc, double a,
+                 double b, const double *pen) {
     switch (nl) {
-        case 1: return kp_st_idx<1>(l, j, bp);
-        case 2: return kp_st_idx<2>(l, j, bp);
-        case 3: return kp_st_idx<3>(l, j, bp);
-        case 4: return kp_st_idx<4>(l, j, bp);
-        case 5: return kp_st_idx<5>(l, j, bp);
-        case 6: return kp_st_idx<6>(l, j, bp);
-        case 7: return kp_st_idx<7>(l, j, bp);
-        default: return kp_st_idx<8>(l, j, bp);
-    }
-}
-
-void cell_values(int nl, uint32_t l, uint32_t npairs, const uint4 *lp, float *st, uint32_t bp, const kp_single_ctx &sc,
-                 double a, double b, const double *pen) {
-    switch (nl) {
-        case 1: kp_dp_cell_list<1, 1>(l, npairs, lp, lp, st, bp, sc, a, b, pen); break;
-        case 2: kp_dp_cell_list<2, 2>(l, npairs, lp, lp, st, bp, sc, a, b, pen); break;
-        case 3: kp_dp_cell_list<3, 3>(l, npairs, lp, lp, st, bp, sc, a, b, pen); break;
-        case 4: kp_dp_cell_list<4, 4>(l, npairs, lp, lp, st, bp, sc, a, b, pen); break;
-        case 5: kp_dp_cell_list<5, 5>(l, npairs, lp, lp, st, bp, sc, a, b, pen); break;
-        case 6: kp_dp_cell_list<6, 6>(l, npairs, lp, lp, st, bp, sc, a, b, pen); break;
-        case 7: kp_dp_cell_list<7, 7>(l, npairs, lp, lp, st, bp, sc, a, b, pen); break;
-        default: kp_dp_cell_list<8, 8>(l, npairs, lp, lp, st, bp, sc, a, b, pen); break;
+        case 1: kp_dp_cell_list<1, 1>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 2: kp_dp_cell_list<2, 2>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 3: kp_dp_cell_list<3, 3>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 4: kp_dp_cell_list<4, 4>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 5: kp_dp_cell_list<5, 5>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 6: kp_dp_cell_list<6, 6>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        case 7: kp_dp_cell_list<7, 7>(l, npairs, lp, lp, st, sc, a, b, pen); break;
+        default: kp_dp_cell_list<8, 8>(l, npairs, lp, lp, st, sc, a, b, pen); break;
     }
 }
 
@@ -108,7 +94,7 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
             int np = kp_high_pairs(g, hp.tabs.data(), h, hpairs.data());
             for (int gi = 0; gi < ngroups; ++gi) {
                 const kp_group_dev &G = groups[gi];
-                st.assign((size_t)G.nl * g.Bpad, 0.0f);  // lane planes (kp_st_idx), like the kernel
+                st.assign((size_t)G.nl * g.Bpad, 0.0f);  // interleaved [cell][lane], like the kernel
                 kp_build_count_table<CT>(g, K.data(), h, G.fold, hp.lowmask.data(), bufA.data(), bufB.data(),
                                          ptab.data(), 0u, 1u, [] {});
                 // gather (values only)
@@ -119,7 +105,7 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
                         for (int p = 0; p < np; ++p)
                             best = fminf(best, S[kp_lane_row(g, hpairs[p].h1, lane) + l] +
                                                    S[kp_lane_row(g, hpairs[p].h2, lane) + l]);
-                        st[st_idx(G.nl, l, ll, g.Bpad)] = l < g.B ? best : __builtin_huge_valf();  // pad slot: +inf
+                        st[(size_t)l * G.nl + ll] = l < g.B ? best : __builtin_huge_valf();  // pad slot: +inf
                     }
                 }
                 // levels (same descriptor table, count table and cell function as kp_dp_kernel)
@@ -138,13 +124,13 @@ int emu(const char *gp, uint32_t max_block, const CT *M, const CT *U, int nf, co
                             sc.log1mp = log(1.0 - p);
                         }
                         const uint4 *lp = reinterpret_cast<const uint4 *>(hp.lpairs.data()) + (D.pl >> 8);
-                        cell_values(G.nl, D.l, D.pl & 0xFFu, lp, st.data(), g.Bpad, sc, G.alpha, G.beta, G.pen);
+                        cell_values(G.nl, D.l, D.pl & 0xFFu, lp, st.data(), sc, G.alpha, G.beta, G.pen);
                     }
                 }
                 // store
                 for (int ll = 0; ll < G.nl; ++ll) {
                     uint64_t row = kp_lane_row(g, h, (uint32_t)G.lane0 + ll);
-                    for (uint32_t l = 0; l < g.Bpad; ++l) S[row + l] = st[st_idx(G.nl, l, ll, g.Bpad)];
+                    for (uint32_t l = 0; l < g.Bpad; ++l) S[row + l] = st[(size_t)l * G.nl + ll];
                 }
             }
         }
