@@ -85,7 +85,10 @@ struct kp_dp_params {
 #define KP_PTAB_ALL (NL == 1)
 #endif
 #ifndef KP_PS
-#define KP_PS 8  // threads per (cell, lane) on a block's narrowest levels (power of 2, <= 64)
+// threads per (cell, lane) on a block's narrowest levels (power of 2, <= 64; 1-lane build only):
+// one wave per (cell, lane) on the levels of <= 8 cells -- 1-lane pass 133.0 -> 127.7 ms
+// (8: 133.0, 16: 129.4, 32: 132.8, 64: 127.7; profiles/r04/experiments/ps_ab.txt)
+#define KP_PS 64
 #endif
 #ifndef KP_NARROW_CHUNKS
 #define KP_NARROW_CHUNKS KP_PRE_CHUNKS  // pair chunks prefetched per cell on lane-split (narrow) levels
