@@ -422,7 +422,7 @@ def full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds=(2, 4, 8)):
     return out
 
 
-def scaling_table(line, cv, prep, npat):
+def scaling_table(line, cv, prep, npat, world=1):
     """patterns scored/s, kernel roofline fraction and CV wall-clock (with and without the
     one-time lane allocation) at every GPU count north_star names: N = 1 measured (the
     line's own step rate and roofline, the full CV run), N = 2, 4, 8 modelled (model_world:
@@ -430,9 +430,10 @@ def scaling_table(line, cv, prep, npat):
     the whole grid's units (cells x folds x (alpha, c)) / CV wall-clock; roofline_frac = the
     sweep kernels' compulsory bytes / their HIP-event time / 8 TB/s, per GPU (min and mean
     over the ranks); weak_units_per_s = N x the measured per-GPU step rate (what the
-    driver's scaling run measures)."""
+    driver's scaling run measures).  Under torchrun (world > 1) the entry of N = world is the
+    measured job itself (wall-clock max over ranks) and nothing is modelled."""
     total = npat * sum(len(g[3]) for g in prep["groups"])
-    out = {"1": {"units_per_s": total / cv["wall_s"], "units_per_s_incl_alloc": total / cv["wall_s_incl_alloc"],
+    out = {str(world): {"units_per_s": total / cv["wall_s"], "units_per_s_incl_alloc": total / cv["wall_s_incl_alloc"],
                  "roofline_frac": line["roofline"]["frac"], "roofline_frac_min": line["roofline"]["frac"],
                  "wall_s": cv["wall_s"], "wall_s_incl_alloc": cv["wall_s_incl_alloc"],
                  "hbm_alloc_s": cv["hbm_alloc_s"], "weak_units_per_s": line["value"], "measured": True}}
@@ -535,6 +536,8 @@ def main():
     if not a.no_full_cv:
         barrier()
         cv = full_cv(plan, prep, gen_pat, rank, world, cap, model_worlds)
+        cv["wall_s_incl_alloc"] = max_over_ranks(cv["wall_s_incl_alloc"])  # (each rank: its wall + its allocation)
+        cv["hbm_alloc_s"] = max_over_ranks(cv["hbm_alloc_s"])
         cv["wall_s"] = max_over_ranks(cv["wall_s"])
 
     units_rank = sum(s["units"] for s in stats)
@@ -607,7 +610,7 @@ def main():
             "kernel_tag": tag,
         }
         if cv:
-            line["scaling_by_gpus"] = scaling_table(line, cv, prep, plan.info["npat"])
+            line["scaling_by_gpus"] = scaling_table(line, cv, prep, plan.info["npat"], world)
             line["hbm_alloc"] = {"lanes": prep["alloc_lanes"], "s": prep["t_alloc"],
                                  "bytes": prep["alloc_lanes"] * plan.info["bytes_per_lane"]}
         if cv and "models" in cv:
