@@ -167,8 +167,8 @@ int kp_math_log(kp_ctx *ctx, const double *x, double *y, uint64_t n);
 
 /* Parity check of the C library's log / log1p as restated for the GPU (kp_libm.h: the
  * sweep's exact fallback, the backtrack and the k-mer terms): fn 1 = log, 2 = log1p
- * (fn 0 = the device's own log, as kp_math_log; fn 3 = kp_fast_log, the sweep's table-free
- * fdlibm log), computed on the context's GPU. */
+ * (fn 0 = the device's own log, as kp_math_log; fn 3 = kp_fast_log, the table-free fdlibm
+ * log; fn 4 = kp_fma_log, its FMA / hardware-reciprocal form), computed on the context's GPU. */
 int kp_math_libm(kp_ctx *ctx, const double *x, double *y, uint64_t n, int fn);
 
 /* --score all_kmers on the context's GPU: one rate per k-mer, no lattice DP

@@ -98,6 +98,8 @@ struct kp_dp_params {
 // -DKP_FAST_LOG, else the device's own (ocml)
 #ifdef KP_FAST_LOG
 #define KP_DLOG(x) kp_fast_log(x)
+#elif defined(KP_FMA_LOG)
+#define KP_DLOG(x) kp_fma_log(x)
 #else
 #define KP_DLOG(x) log(x)
 #endif

@@ -344,10 +344,11 @@ __global__ void __launch_bounds__(256) kp_bt_finish(kp_bt_params P) {
 }
 
 // the C library's log (fn 1) or log1p (fn 2) as restated for the device (kp_libm.h), the
-// device's own log (fn 0), or the table-free fast log (fn 3, kp_fast_log)
+// device's own log (fn 0), the table-free fast log (fn 3, kp_fast_log) or its FMA form (fn 4, kp_fma_log)
 __global__ void kp_libm_kernel(const double *__restrict__ x, double *__restrict__ y, uint64_t n, int fn) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        y[i] = fn == 1 ? kp_libm_log(x[i]) : fn == 2 ? kp_libm_log1p(x[i]) : fn == 3 ? kp_fast_log(x[i]) : log(x[i]);
+        y[i] = fn == 1 ? kp_libm_log(x[i]) : fn == 2 ? kp_libm_log1p(x[i]) : fn == 3 ? kp_fast_log(x[i])
+             : fn == 4 ? kp_fma_log(x[i]) : log(x[i]);
 }
 
 // float32 scores of the given cells of one lane (parity checks of a full-size pass: the
@@ -1505,7 +1506,7 @@ extern "C" {
 int kp_math_log(kp_ctx *c, const double *x, double *y, uint64_t n) { return kp_math_libm(c, x, y, n, 0); }
 
 int kp_math_libm(kp_ctx *c, const double *x, double *y, uint64_t n, int fn) {
-    if (!c || (n && (!x || !y)) || fn < 0 || fn > 3) return fail(KP_E_ARG, "bad arguments");
+    if (!c || (n && (!x || !y)) || fn < 0 || fn > 4) return fail(KP_E_ARG, "bad arguments");
     if (!n) return KP_OK;
     KP_HIP(hipSetDevice(c->device));
     double *dx = nullptr, *dy = nullptr;

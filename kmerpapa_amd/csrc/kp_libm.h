@@ -204,3 +204,51 @@ __host__ __device__ inline double kp_fast_log(double x) {
     const double b = big ? hfsq - (s * (hfsq + R) + dk * ln2_lo) : s * (f - R) - dk * ln2_lo;
     return dk * ln2_hi - (b - f);
 }
+
+// kp_fma_log -- fdlibm's log algorithm (as kp_fast_log) rewritten for throughput on the
+// GPU: the quotient s = f / (2 + f) from the hardware reciprocal refined by Newton steps
+// (no IEEE division sequence), the polynomials and the quotient's correction as fused
+// multiply-adds, fdlibm's k == 0 and small-f branches folded into the general formula
+// (the same values up to rounding), and both of its final formulas evaluated and one
+// selected.  Not bit-identical to fdlibm or the C library: within 2 ulp of the C library's
+// log, which is what the store guard admits (kp_core.h kp_store_unsafe; checked at build
+// time by kp_libm_check on the host's form -- exact reciprocal -- and on the GPU by
+// test_device_fma_log_within_2ulp).  Arguments outside the normal positive range take the
+// C library's restated log (out of line).
+__host__ __device__ inline double kp_fma_log(double x) {
+    const double ln2_hi = 0x1.62e42fee00000p-1, ln2_lo = 0x1.a39ef35793c76p-33;
+    const double Lg1 = 0x1.5555555555593p-1, Lg2 = 0x1.999999997fa04p-2, Lg3 = 0x1.2492494229359p-2,
+                 Lg4 = 0x1.c71c51d8e78afp-3, Lg5 = 0x1.7466496cb03dep-3, Lg6 = 0x1.39a09d078c69fp-3,
+                 Lg7 = 0x1.2f112df3e5244p-3;
+    const uint64_t ix = kp_asu64(x);
+    int32_t hx = (int32_t)(ix >> 32);
+    if (__builtin_expect(hx < 0x00100000 || hx >= 0x7ff00000, 0)) return kp_libm_log(x);
+    int32_t k = (hx >> 20) - 1023;
+    hx &= 0x000fffff;
+    const int32_t i0 = (hx + 0x95f64) & 0x100000;  // mantissa >= sqrt(2): halve it (fdlibm)
+    const double xn = kp_asf64(((uint64_t)(uint32_t)(hx | (i0 ^ 0x3ff00000)) << 32) | (ix & 0xffffffffull));
+    k += (i0 >> 20);
+    const double f = xn - 1.0;  // exact
+    const double d = 2.0 + f;
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(d);  // d in [1.7, 2.5]: no scaling needed
+    r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    r = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+#else
+    const double r = 1.0 / d;
+#endif
+    double s = f * r;
+    s = __builtin_fma(__builtin_fma(-s, d, f), r, s);
+    const double z = s * s;
+    const double w = z * z;
+    const double t1 = w * __builtin_fma(w, __builtin_fma(w, Lg6, Lg4), Lg2);
+    const double t2 = z * __builtin_fma(w, __builtin_fma(w, __builtin_fma(w, Lg7, Lg5), Lg3), Lg1);
+    const double R = t2 + t1;
+    const bool big = ((hx - 0x6147a) | (0x6b851 - hx)) > 0;
+    const double dk = (double)k;
+    const double hfsq = 0.5 * f * f;
+    // fdlibm: big  dk*ln2_hi - ((hfsq - (s*(hfsq+R) + dk*ln2_lo)) - f)
+    //         else dk*ln2_hi - ((s*(f-R) - dk*ln2_lo) - f)          (k == 0: the same with dk = 0)
+    const double b = big ? hfsq - __builtin_fma(s, hfsq + R, dk * ln2_lo) : __builtin_fma(s, f - R, -dk * ln2_lo);
+    return __builtin_fma(dk, ln2_hi, -(b - f));
+}

@@ -553,6 +553,29 @@ def test_device_fast_log_within_1ulp(eng):
     assert np.isneginf(eng.get_device(0).libm(np.array([0.0]), 3)[0])
 
 
+def test_device_fma_log_within_2ulp(eng):
+    """kp_fma_log (fn 4 of kp_math_libm: fdlibm's algorithm with the hardware reciprocal,
+    Newton steps and fused multiply-adds; the sweep's fast-path log in -DKP_FMA_LOG builds)
+    on the GPU against the box's C library: within 2 ulp on the DP's range and across the
+    whole normal range -- the store guard's premise (kp_core.h kp_store_unsafe)."""
+    import ctypes
+    libm = ctypes.CDLL("libm.so.6")
+    libm.log.argtypes = [ctypes.c_double]
+    libm.log.restype = ctypes.c_double
+    rng = np.random.RandomState(9)
+    n = 100_000
+    u = rng.uniform(0.0, 1.0, n)
+    x = np.concatenate([u, 1.0 - u, u * 1e-6, 1.0 - u * 1e-6, 1.0 - rng.uniform(0.0, 0.07, n),
+                        np.exp(rng.uniform(-700.0, 709.0, n)),
+                        np.array([1.0, 2.0, 0.5, 2.2250738585072014e-308, np.nextafter(1.0, 0), np.nextafter(1.0, 2)])])
+    got = eng.get_device(0).libm(x, 4)
+    want = np.array([libm.log(float(v)) for v in x])
+    ulps = np.abs(got.view(np.int64) - want.view(np.int64))
+    assert ulps.max() <= 2, (x[np.argmax(ulps)], ulps.max())
+    special = np.array([0.0, -1.0, np.inf, np.nan, 5e-324])
+    assert np.array_equal(eng.get_device(0).libm(special, 4), eng.get_device(0).libm(special, 1), equal_nan=True)
+
+
 def test_uint64_counts_multilevel_vs_oracle(eng):
     """Counts whose total exceeds 2^32 - 1 take the reference's uint64 itype (CV :94-97):
     the 64-bit count tables and kernels (their larger LDS tables put 4 lanes in a workgroup
