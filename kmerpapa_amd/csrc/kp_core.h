@@ -103,6 +103,12 @@ struct kp_lowdesc {
     uint32_t pl;     // low split pairs: (first 4-pair chunk in kp_plan's lpairs) << 8 | count
 };
 
+// a block's high split pair (child blocks h - d1 and h - d2, at high position pos) as one
+// word of the plan's hpd table (d1, d2 < 2^29 blocks)
+__host__ __device__ inline uint64_t kp_hpd_word(uint64_t d1, uint64_t d2, uint32_t pos) {
+    return d1 | (d2 << 29) | ((uint64_t)pos << 58);
+}
+
 // ---------------------------------------------------------------------------
 // scoring arithmetic (float64, order of operations as in the reference)
 // ---------------------------------------------------------------------------

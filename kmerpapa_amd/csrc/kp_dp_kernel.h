@@ -29,6 +29,11 @@ struct kp_dev_tables {
     const uint32_t *kpos;  // block -> its position in the block list = its count row of K
     const uint8_t *lowmask;
     const uint4 *lpairs;  // low split-pair lists in 4-pair chunks (kp_plan.h lpairs)
+    // [block list][hps] the block's high split pairs in scan order as kp_hpd_word (child
+    // block deltas + position), built once per plan by kp_hpd_kernel; null when a block
+    // can have more than 64 pairs (then the pairs come from hdig / tabs)
+    const uint64_t *hpd;
+    uint32_t hps;
 };
 
 struct kp_dp_params {
@@ -306,6 +311,27 @@ kp_dp_kernel(kp_dp_params P) {
             if ((P.ntmask >> i) & 1u) nnt += npi;
         }
     const uint64_t rowstride = (uint64_t)g.Ltot * Bpad;
+    if (P.T.hpd) {
+        // wave 0, lane p = pair p: its child-block deltas come in one load that needs neither
+        // h nor the pair counts (the padding words past np are loaded and unused), so the
+        // block setup costs one dependent round trip, not two; the non-temporal positions'
+        // pairs go first (slot = rank among the pairs of the same kind)
+        if (threadIdx.x < 64) {
+            const uint32_t p = threadIdx.x;
+            const uint64_t e = p < P.T.hps ? P.T.hpd[(P.hbase + widx) * P.T.hps + p] : 0;
+            const bool valid = (int)p < np;
+            const uint32_t pos = (uint32_t)(e >> 58);
+            const bool ntp = valid && ((P.ntmask >> pos) & 1u);
+            const uint64_t bnt = __ballot(ntp), bv = __ballot(valid);
+            const uint64_t below = (1ull << p) - 1ull;
+            if (valid) {
+                const int slot = ntp ? __popcll(bnt & below) : nnt + __popcll(bv & ~bnt & below);
+                hp[slot].h1 = (h - (e & 0x1FFFFFFFull)) * rowstride;  // child rows as element offsets of lane 0
+                hp[slot].h2 = (h - ((e >> 29) & 0x1FFFFFFFull)) * rowstride;
+                hp[slot].code = pos;
+            }
+        }
+    } else
     for (int p = (int)threadIdx.x; threadIdx.x < 64 && p < np; p += 64) {  // wave 0
         // pair p in scan order; slot: the non-temporal positions' pairs first (the sweep
         // only takes a min, so pair order does not matter here)

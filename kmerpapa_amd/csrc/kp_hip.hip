@@ -343,6 +343,28 @@ __global__ void __launch_bounds__(256) kp_bt_finish(kp_bt_params P) {
     }
 }
 
+// The high split pairs of every block of the block list, in scan order (positions
+// ascending, pairs in table order: the order kp_dp_kernel's pair setup walks them), as
+// child-block deltas: hpd[q][0 .. np) = kp_hpd_word, the rest of the hps-word row 0.  One
+// thread per block, once per plan.
+__global__ void kp_hpd_kernel(kp_geom g, const kp_postab *__restrict__ tabs, const uint64_t *__restrict__ hdig,
+                              uint64_t nblocks, uint32_t hps, uint64_t *__restrict__ hpd) {
+    for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < nblocks;
+         q += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t hd = hdig[q];
+        uint64_t *row = hpd + q * hps;
+        uint32_t n = 0;
+        for (int i = 0; i < g.kh; ++i) {
+            const kp_postab &T = tabs[g.t + i];
+            const uint32_t d = (uint32_t)(hd >> (4 * i)) & 15u;
+            for (uint32_t r = 0; r < T.np[d]; ++r)
+                row[n++] = kp_hpd_word((uint64_t)(d - T.pa[d][r]) * g.hcg[i], (uint64_t)(d - T.pb[d][r]) * g.hcg[i],
+                                       (uint32_t)i);
+        }
+        for (; n < hps; ++n) row[n] = 0;
+    }
+}
+
 // the C library's log (fn 1) or log1p (fn 2) as restated for the device (kp_libm.h), the
 // device's own log (fn 0), the table-free fast log (fn 3, kp_fast_log) or its FMA form (fn 4, kp_fma_log)
 __global__ void kp_libm_kernel(const double *__restrict__ x, double *__restrict__ y, uint64_t n, int fn) {
@@ -424,6 +446,8 @@ struct kp_plan {
     kp_lowdesc *d_ldesc = nullptr;
     uint64_t *d_hdig = nullptr;
     uint64_t *d_hnp = nullptr;
+    uint64_t *d_hpd = nullptr;  // [nblocks][hps] high split pairs per block (kp_hpd_kernel)
+    uint32_t hps = 0;
     uint8_t *d_lowmask = nullptr;
     uint32_t *d_lpairs = nullptr;
     // counts
@@ -477,6 +501,8 @@ static kp_dev_tables tables_of(const kp_plan *p) {
     T.ldesc = p->d_ldesc;
     T.hdig = p->d_hdig;
     T.hnp = p->d_hnp;
+    T.hpd = p->d_hpd;
+    T.hps = p->hps;
     T.lowmask = p->d_lowmask;
     T.lpairs = reinterpret_cast<const uint4 *>(p->d_lpairs);
     return T;
@@ -583,6 +609,28 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
         kp_plan_destroy(p);
         return rc;
     }
+    // the blocks' high split pairs as child-block deltas (one load per pair in the sweep's
+    // block setup); only when every block has at most 64 pairs (one wave) and the deltas
+    // fit their 29-bit fields -- otherwise the sweep derives them from hdig and tabs
+    {
+        const kp_geom &g = p->hp.g;
+        uint32_t most = 0;
+        for (int i = 0; i < g.kh; ++i) {
+            uint32_t m = 0;
+            for (uint32_t d = 0; d < g.r[g.t + i]; ++d) m = std::max<uint32_t>(m, p->hp.tabs[g.t + i].np[d]);
+            most += m;
+        }
+        const char *e = getenv("KP_HPD");
+        if ((!e || atoi(e) != 0) && most >= 1 && most <= 64 && g.nblocks < (1ull << 29)) {
+            p->hps = most;
+            KP_HIP(dmalloc(&p->d_hpd, g.nblocks * most * sizeof(uint64_t)));
+            const unsigned nb = (unsigned)std::min<uint64_t>((g.nblocks + 255) / 256, 16384);
+            hipLaunchKernelGGL(kp_hpd_kernel, dim3(nb), dim3(256), 0, ctx->stream, g, p->d_tabs, p->d_hdig,
+                               (uint64_t)g.nblocks, most, p->d_hpd);
+            KP_HIP(hipGetLastError());
+            KP_HIP(hipStreamSynchronize(ctx->stream));
+        }
+    }
     *out = p;
     return KP_OK;
 }
@@ -592,7 +640,7 @@ void kp_plan_destroy(kp_plan *p) {
     if (p->ctx) (void)hipSetDevice(p->ctx->device);
     free_scores(p);
     void *bufs[] = {p->d_tabs,    p->d_lowinfo, p->d_loff,   p->d_klofs,   p->d_kllist, p->d_hlist, p->d_kpos, p->d_ldesc,
-                    p->d_hdig,    p->d_hnp,     p->d_lowmask, p->d_lpairs, p->d_K,      p->d_nodes, p->d_groups,
+                    p->d_hdig,    p->d_hnp,     p->d_hpd,     p->d_lowmask, p->d_lpairs, p->d_K,      p->d_nodes, p->d_groups,
                     p->d_lanegrp, p->d_rtrain,  p->d_rtest,  p->d_nleaves, p->d_bad,    p->d_cnt,   p->d_dend,
                     p->d_leaves};
     if (p->cstream) (void)hipStreamSynchronize(p->cstream);
