@@ -99,15 +99,29 @@ struct kp_dp_params {
 #define KP_NARROW_CHUNKS KP_PRE_CHUNKS  // pair chunks prefetched per cell on lane-split (narrow) levels
 #endif
 
-// the fast path's float64 log (kp_libm.h): kp_fast_log (fdlibm, table-free) with
-// -DKP_FAST_LOG, else the device's own (ocml)
-#ifdef KP_FAST_LOG
-#define KP_DLOG(x) kp_fast_log(x)
-#elif defined(KP_FMA_LOG)
-#define KP_DLOG(x) kp_fma_log(x)
-#else
-#define KP_DLOG(x) log(x)
+// the fast path's float64 log (within 2 ulp of the C library's: the store guard, kp_core.h
+// kp_store_unsafe, sends every result that could depend on it to the C library's restated
+// log).  Builds of NL lanes with bit NL of KP_FMA_LOG_MASK set take kp_fma_log (kp_libm.h:
+// fdlibm's algorithm with the hardware reciprocal and FMAs, ~45 instructions against
+// ocml's ~80 of double-double arithmetic): 1-lane pass 125 -> 113 ms, 5-lane 379 -> 377;
+// the 2- and 3-lane builds (80 VGPRs at 6 waves per SIMD) keep the device's own log (ocml),
+// their spills grow with it (3 lanes 247 -> 283 ms; profiles/r04/experiments/fmalog_ab.txt).
+// -DKP_FAST_LOG: kp_fast_log (fdlibm, IEEE division) in every build (A/B only).
+#ifndef KP_FMA_LOG_MASK
+#define KP_FMA_LOG_MASK 0x1F2u  // NL = 1, 4, 5, 6, 7, 8
 #endif
+template <int NL>
+__device__ inline double kp_dlog(double x) {
+#ifdef KP_FAST_LOG
+    return kp_fast_log(x);
+#else
+    if constexpr (((KP_FMA_LOG_MASK) >> NL) & 1u)
+        return kp_fma_log(x);
+    else
+        return log(x);
+#endif
+}
+#define KP_DLOG(x) kp_dlog<NL>(x)
 
 // v[j] of a small register array for a per-lane j, as a select chain (no memory access)
 template <int N>
