@@ -249,6 +249,9 @@ __host__ __device__ inline double kp_fma_log(double x) {
     const double hfsq = 0.5 * f * f;
     // fdlibm: big  dk*ln2_hi - ((hfsq - (s*(hfsq+R) + dk*ln2_lo)) - f)
     //         else dk*ln2_hi - ((s*(f-R) - dk*ln2_lo) - f)          (k == 0: the same with dk = 0)
-    const double b = big ? hfsq - __builtin_fma(s, hfsq + R, dk * ln2_lo) : __builtin_fma(s, f - R, -dk * ln2_lo);
+    // as one expression b = a0 - (s*b0 + dk*ln2_lo): for "else" a0 = 0, b0 = R - f, and
+    // 0 - fma(s, R - f, c) is fma(s, f - R, -c) exactly (negation is exact, rounding symmetric)
+    const double a0 = big ? hfsq : 0.0, b0 = big ? hfsq + R : R - f;
+    const double b = a0 - __builtin_fma(s, b0, dk * ln2_lo);
     return __builtin_fma(dk, ln2_hi, -(b - f));
 }
