@@ -101,27 +101,32 @@ struct kp_dp_params {
 
 // the fast path's float64 log (within 2 ulp of the C library's: the store guard, kp_core.h
 // kp_store_unsafe, sends every result that could depend on it to the C library's restated
-// log).  Builds of NL lanes with bit NL of KP_FMA_LOG_MASK set take kp_fma_log (kp_libm.h:
-// fdlibm's algorithm with the hardware reciprocal and FMAs, ~45 instructions against
-// ocml's ~80 of double-double arithmetic): 1-lane pass 125 -> 113 ms, 5-lane 379 -> 377;
-// the 2- and 3-lane builds (80 VGPRs at 6 waves per SIMD) keep the device's own log (ocml),
-// their spills grow with it (3 lanes 247 -> 283 ms; profiles/r04/experiments/fmalog_ab.txt).
+// log).  Single-alpha builds of NL lanes with bit NL of KP_FMA_LOG_MASK set take
+// kp_fma_log (kp_libm.h: fdlibm's algorithm with the hardware reciprocal and FMAs, ~45
+// instructions against ocml's ~80 of double-double arithmetic): pass 1 lane 124.3 -> 111.1
+// ms, 4 lanes 317.9 -> 312.3, 5 lanes 380.3 -> 377.0.  The 2- and 3-lane builds (80 VGPRs at
+// 6 waves per SIMD) and the mixed-group builds (two rates, four logs per cell) keep the
+// device's own log (ocml): with kp_fma_log their spills grow (3 lanes 248 -> 284 ms, 2 lanes
+// 179 -> 206, mixed 2 + 3 lanes 404 -> 409; profiles/r04/experiments/fmalog_ab.txt).
 // -DKP_FAST_LOG: kp_fast_log (fdlibm, IEEE division) in every build (A/B only).
 #ifndef KP_FMA_LOG_MASK
 #define KP_FMA_LOG_MASK 0x1F2u  // NL = 1, 4, 5, 6, 7, 8
 #endif
-template <int NL>
+#ifndef KP_FMA_LOG_MIX
+#define KP_FMA_LOG_MIX 0  // 1: the mixed builds too (A/B)
+#endif
+template <int NL, bool MIX>
 __device__ inline double kp_dlog(double x) {
 #ifdef KP_FAST_LOG
     return kp_fast_log(x);
 #else
-    if constexpr (((KP_FMA_LOG_MASK) >> NL) & 1u)
+    if constexpr ((((KP_FMA_LOG_MASK) >> NL) & 1u) && (!MIX || KP_FMA_LOG_MIX))
         return kp_fma_log(x);
     else
         return log(x);
 #endif
 }
-#define KP_DLOG(x) kp_dlog<NL>(x)
+#define KP_DLOG(x) kp_dlog<NL, MIX>(x)
 
 // v[j] of a small register array for a per-lane j, as a select chain (no memory access)
 template <int N>
