@@ -310,6 +310,13 @@ __host__ __device__ inline bool kp_store_unsafe(double s) {
     return ((lo + 64u) & 0x1FFFFF80u) == 0x10000000u;
 }
 
+// The reference's store of a single-pattern term (CV :71-72): `if s < best: best = f32(s)`,
+// s float64, best float32.  Rounding to nearest is monotone, so f32(s) <= best exactly when
+// s < best or f32(s) == best, and min(f32(s), best) is that same store in one float32 min
+// (no float64 compare); a NaN s drops out of fminf as it fails the compare (best is never
+// NaN: split candidates enter through fminf too, and every score is >= +0).
+__host__ __device__ inline float kp_store_min(double s, float best) { return fminf((float)s, best); }
+
 // the fast path's premise (kp_store_unsafe): penalties, alpha and beta not negative, and
 // beta either 0 or not so small that a single term could fall below float32's normal range
 __host__ __device__ inline bool kp_fast_logs_ok(const double *pen, int n, double alpha, double beta) {
@@ -330,7 +337,7 @@ __host__ __device__ inline void kp_cell_store(SP row, const float *lmin, const k
         for (int j = 0; j < W; ++j) {
             const bool s2 = (int)(j0 + j) >= sc.js;
             const double s = kp_single_train(sc.c, s2 ? sc.logp2 : sc.logp, s2 ? sc.log1mp2 : sc.log1mp, pen[j]);
-            out[j] = s < (double)lmin[j] ? (float)s : lmin[j];
+            out[j] = kp_store_min(s, lmin[j]);
             unsafe = unsafe || kp_store_unsafe(s);
         }
     } else {
@@ -338,7 +345,7 @@ __host__ __device__ inline void kp_cell_store(SP row, const float *lmin, const k
         for (int j = 0; j < W; ++j) {
             const bool s2 = MIX && (int)(j0 + j) >= sc.js;
             const double s = kp_single_train(sc.c, s2 ? sc.logp2 : sc.logp, s2 ? sc.log1mp2 : sc.log1mp, pen[j]);
-            out[j] = s < (double)lmin[j] ? (float)s : lmin[j];  // float64 compare against the float32 store (CV :71)
+            out[j] = kp_store_min(s, lmin[j]);  // the float64 compare against the float32 store (CV :71)
         }
 #pragma unroll
         for (int j = 0; j < W; ++j) {  // (every lane, stored or not: cheaper than telling them apart)
@@ -361,7 +368,7 @@ __host__ __device__ inline void kp_cell_store(SP row, const float *lmin, const k
             const bool s2 = MIX && (int)(j0 + j) >= sc.js;
             float best = lmin[j];
             const double v = kp_single_train(sc.c, s2 ? lp2 : lp, s2 ? l1p2 : l1p, pen[j]);
-            if (v < (double)best) best = (float)v;
+            best = kp_store_min(v, best);
             out[j] = best;
         }
     }
