@@ -423,19 +423,72 @@ __host__ __device__ inline void kp_dp_cell_values(const kp_geom &g, WP pw, uint3
     kp_cell_store<W>(row, lmin, sc, pen, alpha, beta);
 }
 
+// Pair-list decode of the SDWA builds (kp_sdwa_on): the byte offset K * (half HI of a
+// pair-list word) = c * NL * 4 for a child cell c is one v_mul_u32_u24 whose source
+// operand selects the 16-bit half, and the LDS read takes it as its address (the dynamic
+// LDS array starts at address 0: the kernels declare no static LDS, checked at launch,
+// kp_hip.hip launch_dp_hz).  The plain form (mask or shift, multiply-add, add of the array
+// base) costs 3 VALU per child instead of 1.  Per build, as measured
+// (profiles/r04/experiments/sdwa_ab.txt): 1 lane 111.5 -> 109.1 ms, 3 lanes 251 -> 243,
+// mixed 5 lanes 402 -> 399; 5 lanes unchanged, 4 lanes 311 -> 326 (register allocation).
+// Bit NL of the mask = the NL-lane build, bit 0 = the mixed builds.
+#ifndef KP_SDWA_MASK
+#define KP_SDWA_MASK 0x0Fu  // mixed, 1, 2, 3 lanes
+#endif
+template <int NL, bool MIX>
+__host__ __device__ constexpr bool kp_sdwa_on() {
+    return ((KP_SDWA_MASK >> (MIX ? 0 : NL)) & 1u) != 0;
+}
+
+template <uint32_t K, int HI>
+__host__ __device__ inline uint32_t kp_half_mul(uint32_t e) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    static_assert(K <= 64, "inline constant");
+    uint32_t r;
+    if constexpr (HI)
+        asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD"
+            : "=v"(r) : "v"(e), "i"(K));
+    else
+        asm("v_mul_u32_u24_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD"
+            : "=v"(r) : "v"(e), "i"(K));
+    return r;
+#else
+    return (HI ? e >> 16 : e & 0xFFFFu) * K;
+#endif
+}
+
+// the float at byte offset off of the LDS row array (device: LDS address off) / of a
+// host array st
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ inline float kp_at_bytes(__attribute__((address_space(3))) float *, uint32_t off) {
+    return *(__attribute__((address_space(3))) float *)(uintptr_t)off;
+}
+#endif
+template <typename SP>
+__host__ __device__ inline float kp_at_bytes(SP st, uint32_t off) { return st[off / 4u]; }
+
 // min over one 4-pair chunk of a cell's split-pair list (c1 | c2 << 16 per pair, kp_plan.h
 // lpairs) for W lanes from j0; all 8*W LDS reads issue before the first min
-template <int NL, int W, int NPC = 4, typename SP>
+template <int NL, int W, int NPC = 4, bool SDWA = false, typename SP>
 __host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0, float *lmin) {
     const uint32_t e[4] = {c.x, c.y, c.z, c.w};
     float va[4][W], vb[4][W];
 #pragma unroll
     for (int p = 0; p < NPC; ++p) {
-        const uint32_t c1 = e[p] & 0xFFFFu, c2 = e[p] >> 16;
+        if constexpr (SDWA) {
+            const uint32_t o1 = kp_half_mul<4u * NL, 0>(e[p]), o2 = kp_half_mul<4u * NL, 1>(e[p]);
 #pragma unroll
-        for (int j = 0; j < W; ++j) {
-            va[p][j] = st[c1 * NL + j0 + j];
-            vb[p][j] = st[c2 * NL + j0 + j];
+            for (int j = 0; j < W; ++j) {
+                va[p][j] = kp_at_bytes(st, o1 + 4u * (j0 + j));
+                vb[p][j] = kp_at_bytes(st, o2 + 4u * (j0 + j));
+            }
+        } else {
+            const uint32_t c1 = e[p] & 0xFFFFu, c2 = e[p] >> 16;
+#pragma unroll
+            for (int j = 0; j < W; ++j) {
+                va[p][j] = st[c1 * NL + j0 + j];
+                vb[p][j] = st[c2 * NL + j0 + j];
+            }
         }
     }
 #pragma unroll
@@ -472,16 +525,16 @@ __host__ __device__ inline void kp_dp_cell_list(uint32_t l, uint32_t npairs, con
     for (int k = 0; k < PRE; ++k)
         if (4u * k < npairs) {
             if (npairs - 4u * k > 2u)
-                kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
+                kp_chunk_minv<NL, W, 4, kp_sdwa_on<NL, MIX>()>(st, pre[k], j0, lmin);
             else
-                kp_chunk_minv<NL, W, 2>(st, pre[k], j0, lmin);
+                kp_chunk_minv<NL, W, 2, kp_sdwa_on<NL, MIX>()>(st, pre[k], j0, lmin);
         }
-    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W, 4, kp_sdwa_on<NL, MIX>()>(st, lp[k], j0, lmin);
 #else
 #pragma unroll
     for (int k = 0; k < PRE; ++k)
-        if (4u * k < npairs) kp_chunk_minv<NL, W>(st, pre[k], j0, lmin);
-    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W>(st, lp[k], j0, lmin);
+        if (4u * k < npairs) kp_chunk_minv<NL, W, 4, kp_sdwa_on<NL, MIX>()>(st, pre[k], j0, lmin);
+    for (uint32_t k = PRE; 4u * k < npairs; ++k) kp_chunk_minv<NL, W, 4, kp_sdwa_on<NL, MIX>()>(st, lp[k], j0, lmin);
 #endif
     kp_cell_store<W, MIX>(row, lmin, sc, pen, alpha, beta, j0);
 }

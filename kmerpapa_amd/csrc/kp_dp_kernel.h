@@ -291,8 +291,9 @@ kp_dp_kernel(kp_dp_params P) {
     //      (count-table scratch aliases st, which the gather fills afterwards; every carve
     //       offset is a multiple of 16 bytes)
     const size_t st_bytes = (size_t)NL * Bpad * 4, scr_bytes = (size_t)P.pscratch_entries * 4 * sizeof(CT);
-    float *st = reinterpret_cast<float *>(smem);
-    CT *ptab = reinterpret_cast<CT *>(smem + (st_bytes > scr_bytes ? st_bytes : ((scr_bytes + 15) & ~(size_t)15)));
+    unsigned char *lbase = smem;
+    float *st = reinterpret_cast<float *>(lbase);
+    CT *ptab = reinterpret_cast<CT *>(lbase + (st_bytes > scr_bytes ? st_bytes : ((scr_bytes + 15) & ~(size_t)15)));
     kp_hpair *hp = reinterpret_cast<kp_hpair *>(ptab + (((size_t)P.ptab_entries * 2 + 3) & ~(size_t)3));
     uint8_t *lm = reinterpret_cast<uint8_t *>(hp + (g.kh * 7 + 1));
 #ifdef KP_STAMPS
@@ -376,8 +377,8 @@ kp_dp_kernel(kp_dp_params P) {
     // (kp_kl_counts of the preloaded row: train = all data - fold, CV :22-24)
     const uint64_t kte_m = fold >= 0 ? (uint64_t)kraw[2] : 0, kte_u = fold >= 0 ? (uint64_t)kraw[3] : 0;
     const kp_cnt kpre = {(uint64_t)kraw[0] - kte_m, (uint64_t)kraw[1] - kte_u, kte_m, kte_u};
-    kp_build_count_table<CT>(g, K, krow, fold, lm, reinterpret_cast<CT *>(smem),
-                             reinterpret_cast<CT *>(smem) + (size_t)P.pscratch_entries * 2, ptab, threadIdx.x,
+    kp_build_count_table<CT>(g, K, krow, fold, lm, reinterpret_cast<CT *>(lbase),
+                             reinterpret_cast<CT *>(lbase) + (size_t)P.pscratch_entries * 2, ptab, threadIdx.x,
                              blockDim.x, [] { __syncthreads(); }, &kpre);
     __syncthreads();
     KP_STAMP(0);
@@ -457,7 +458,7 @@ kp_dp_kernel(kp_dp_params P) {
                 const uint4 *lp = P.T.lpairs + (cur[0].w >> 8);
                 const uint32_t nch = (npairs + 3u) >> 2;
                 for (uint32_t c = (uint32_t)r; c < nch; c += KP_PS)
-                    kp_chunk_minv<NL, 1>((kp_lds_f32 *)st, lp[c], j, &part);
+                    kp_chunk_minv<NL, 1, 4, kp_sdwa_on<NL, MIX>()>((kp_lds_f32 *)st, lp[c], j, &part);
 #pragma unroll
                 for (int m = 1; m < KP_PS; m <<= 1) part = fminf(part, __shfl_xor(part, m, KP_PS));
                 if (r == 0) {

@@ -869,6 +869,16 @@ static size_t dp_lds_bytes(const kp::host_plan &hp, int nl, size_t ct_bytes) {
 
 template <typename CT, int NL, bool HZ, bool MIX>
 static int launch_dp_hz(hipStream_t st, const kp_dp_params &P, unsigned nb, unsigned ngroups, int threads, size_t lds) {
+    if constexpr (kp_sdwa_on<NL, MIX>()) {  // its scan reads the row array at LDS address 0 (kp_at_bytes)
+        static std::atomic<bool> checked{false};
+        if (!checked.load(std::memory_order_relaxed)) {
+            hipFuncAttributes fa;
+            KP_HIP(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&kp_dp_kernel<CT, NL, HZ, MIX>)));
+            if (fa.sharedSizeBytes != 0)
+                return fail(KP_E_HIP, "kp_dp_kernel has static LDS: its dynamic LDS does not start at address 0");
+            checked.store(true, std::memory_order_relaxed);
+        }
+    }
     if (lds > 65536)
         KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_kernel<CT, NL, HZ, MIX>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
