@@ -2,8 +2,10 @@
 tests/test_gpu_parity.py's random cases).  Random IUPAC general patterns (k = 3..6, at
 most two N), random counts (zeros included), folds, pseudo counts, 1-8 penalties, block
 sizes and lanes per workgroup; every cell's float32 score and every root test value must
-equal the oracle's bit for bit.  usage: python tools/parity_sweep.py N_CASES SEED  (SWEEP_MAX_CELLS bounds the lattice;
-SWEEP_U64=1 scales the counts past 2^32 so that every case takes the uint64 itype)"""
+equal the oracle's bit for bit.  usage: python tools/parity_sweep.py N_CASES SEED  (SWEEP_MAX_CELLS bounds the lattice, SWEEP_K lists the pattern lengths;
+SWEEP_U64=1 scales the counts past 2^32 so that every case takes the uint64 itype).  Half the
+cases run two alphas per fold, so that the library cuts their lanes into mixed device groups
+(two (alpha, beta) sets in one workgroup, the MIX builds)"""
 import os
 import random
 import sys
@@ -21,10 +23,11 @@ from oracle import oracle as O  # noqa: E402
 
 MAX_CELLS = int(os.environ.get("SWEEP_MAX_CELLS", "300000"))
 U64 = os.environ.get("SWEEP_U64") == "1"
+KS = [int(x) for x in os.environ.get("SWEEP_K", "3,4,5,6,7").split(",")]  # pattern lengths drawn from
 
 
 def case(rng):
-    k = rng.choice([3, 4, 5, 6, 7])
+    k = rng.choice(KS)
     while True:
         gp = "".join(rng.choice("MRSWKYACGTBDHVNNN") for _ in range(k))
         if np.prod([len(perm_code[c]) for c in gp]) <= MAX_CELLS:
@@ -55,29 +58,31 @@ def main():
         itype = np.uint64 if U64 else np.uint32
         contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(i), itype)
         Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), itype)
-        alpha = rng.choice([0.0, 0.1, 1.0, 7.0])
+        alphas = rng.sample([0.0, 0.1, 1.0, 7.0], rng.choice([1, 2]))
         tot_m = Mf.sum(axis=0).astype(np.uint64)
         tot_u = Uf.sum(axis=0).astype(np.uint64)
         mtr, utr = tot_m.sum() - tot_m, tot_u.sum() - tot_u
         with np.errstate(divide="ignore", invalid="ignore"):
-            betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+            betas = {a: (a * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr)) for a in alphas}
         pens = sorted(rng.sample([0.0, 0.7, 2.0, 3.3, 5.0, 8.0, 13.0, 21.0], rng.randint(1, 8)))
         plan = eng.Plan(dev, gp, rng.choice([0, 0, 16, 64, 512, 2048]))
         plan.set_counts(Mk, Uk)
         try:
-            _, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
-            for pi, c in enumerate(pens):
-                ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, 64 if U64 else 32)
-                for f in range(nf):
-                    lane = f * len(pens) + pi
-                    score, _ = plan.dump_lane(lane)
-                    ok = np.array_equal(np.asarray(score).view(np.uint32), ref["score"][:, f].view(np.uint32)) and \
-                        np.float32(re[lane]).tobytes() == np.float32(ref["root_test"][f]).tobytes()
-                    if not ok:
-                        bad += 1
-                        print("MISMATCH", i, gp, nf, alpha, c, f, flush=True)
+            groups = [(f, a, float(betas[a][f]), pens) for f in range(nf) for a in alphas]
+            _, re, _ = plan.run(groups)
+            for ai, alpha in enumerate(alphas):
+                for pi, c in enumerate(pens):
+                    ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas[alpha], c, 64 if U64 else 32)
+                    for f in range(nf):
+                        lane = (f * len(alphas) + ai) * len(pens) + pi
+                        score, _ = plan.dump_lane(lane)
+                        ok = np.array_equal(np.asarray(score).view(np.uint32), ref["score"][:, f].view(np.uint32)) and \
+                            np.float32(re[lane]).tobytes() == np.float32(ref["root_test"][f]).tobytes()
+                        if not ok:
+                            bad += 1
+                            print("MISMATCH", i, gp, nf, alpha, c, f, flush=True)
         except eng.KPError as e:
-            print("error", i, gp, alpha, e, flush=True)
+            print("error", i, gp, alphas, e, flush=True)
             bad += 1
         plan.close()
         if i % 20 == 0:
