@@ -2,7 +2,8 @@
 skipped.  Needs the timing-ablation build (make -C kmerpapa_amd/csrc ablation) and
 KMERPAPA_LIB=kmerpapa_amd/libkmerpapa_hip_ablation.so; every ablated pass returns
 KP_E_STATE (its numbers are invalid) after recording its timings.
-usage: python tools/ablate.py SKIP [SKIP ...]   (KP_DEBUG_SKIP bit sets, 0 = full pass)
+usage: python tools/ablate.py SKIP [SKIP ...]   (KP_DEBUG_SKIP bit sets, 0 = full pass;
+  ABLATE_LANES=n: a pass of the group's first n penalties, default 5)
   1 = no gather, 2 = no level phase, 4 = no float64 logs, 8 = no low split scan,
   16 = no level barriers"""
 import json
@@ -18,6 +19,7 @@ plan = engine.get_plan(0, "NNNNMNNNN")
 plan.set_counts(prep["Mk"], prep["Uk"])
 plan.reserve(5)
 g = prep["groups"][0]
+g = (g[0], g[1], g[2], list(g[3])[:int(os.environ.get("ABLATE_LANES", "5"))])
 for skip in sys.argv[1:] or ["0"]:
     os.environ["KP_DEBUG_SKIP"] = skip
     ms = []

@@ -6,7 +6,7 @@ import os
 import sys
 
 d = sys.argv[1]
-cells_lanes = 7688671875 * 5
+cells_lanes = 7688671875 * int(os.environ.get("ABLATE_LANES", "5"))
 print("skip  " + "  ".join(f"{c:>22}" for c in ("SQ_INSTS_VALU/unit", "SQ_INSTS_LDS/unit", "SQ_ACTIVE_INST_VALU",
                                                    "LDS_BANK_CONFLICT", "LDS_IDX_ACTIVE")))
 for sub in sorted(glob.glob(os.path.join(d, "s*"))):
