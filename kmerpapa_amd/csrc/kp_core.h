@@ -469,8 +469,20 @@ __host__ __device__ inline float kp_at_bytes(SP st, uint32_t off) { return st[of
 
 // min over one 4-pair chunk of a cell's split-pair list (c1 | c2 << 16 per pair, kp_plan.h
 // lpairs) for W lanes from j0; all 8*W LDS reads issue before the first min
+// KP_CHUNK_SPLIT: builds whose threads scan W >= KP_CHUNK_SPLIT lanes run a 4-pair chunk as
+// two 2-pair halves (4*W LDS values in flight instead of 8*W; the same minima in the same
+// order): 5 lanes 374.6 -> 373.9 ms, mixed 2 + 3 lanes 396.9 -> 395.7, 4 lanes (not split)
+// 308.6 -> 309.5 with it (profiles/r04/experiments/chunk_split_ab.txt)
+#ifndef KP_CHUNK_SPLIT
+#define KP_CHUNK_SPLIT 5
+#endif
 template <int NL, int W, int NPC = 4, bool SDWA = false, typename SP>
 __host__ __device__ inline void kp_chunk_minv(SP st, const uint4 c, uint32_t j0, float *lmin) {
+    if constexpr (NPC == 4 && W >= KP_CHUNK_SPLIT) {
+        kp_chunk_minv<NL, W, 2, SDWA>(st, c, j0, lmin);
+        kp_chunk_minv<NL, W, 2, SDWA>(st, make_uint4(c.z, c.w, c.z, c.w), j0, lmin);
+        return;
+    }
     const uint32_t e[4] = {c.x, c.y, c.z, c.w};
     float va[4][W], vb[4][W];
 #pragma unroll
