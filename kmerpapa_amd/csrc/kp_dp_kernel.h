@@ -49,7 +49,7 @@ struct kp_dp_params {
                                           // not vector loads whose waits stalled every level's start)
     uint32_t ptab_entries;     // separable count table entries (kp_plan.h)
     uint32_t pscratch_entries; // largest intermediate table of its build
-    int remap;  // block -> XCD mapping: G > 1 = runs of G list entries per XCD (default 24),
+    int remap;  // block -> XCD mapping: G > 1 = runs of G list entries per XCD (default 40),
                 // 1 = XCD-contiguous (7 % slower), 0 = hardware round-robin
     int lanesplit;  // split a cell's lanes over threads on narrow levels (KP_LANE_SPLIT=0 disables)
     int ntstore;    // 1 = score rows stored non-temporally (default; KP_NT_STORE=0 for plain stores)

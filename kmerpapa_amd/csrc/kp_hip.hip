@@ -1216,11 +1216,12 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
 #else
     P.dbg = 0;  // the product build has no phase-skipping path
 #endif
-    // runs of 24 consecutive blocks per XCD (workgroups are dealt round-robin over the 8
+    // runs of 40 consecutive blocks per XCD (workgroups are dealt round-robin over the 8
     // XCDs): neighbours in the reuse order share their L2; measured -1 % against none
-    // (DESIGN.md §5), 16 against 8 -1.5 ms per 5-lane pass (12: -1.2, 32: -0.4) and 24
-    // against 16 -1 ms (20: -0.5; profiles/r04/experiments/remap_ab.txt)
-    P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 24;
+    // (DESIGN.md §5), 16 against 8 -1.5 ms per 5-lane pass (12: -1.2, 32: -0.4), 24 against
+    // 16 -1 ms (20: -0.5) and 40 against 24 -1 ms (32: +2, 64: +5; non-monotonic;
+    // profiles/r04/experiments/remap_ab.txt)
+    P.remap = getenv("KP_XCD_REMAP") ? atoi(getenv("KP_XCD_REMAP")) : 40;
     P.lanesplit = getenv("KP_LANE_SPLIT") ? atoi(getenv("KP_LANE_SPLIT")) : 1;
     // KP_EXACT_LOGS=1: no fast device log at all (same results; exercises the exact path)
     P.exact = getenv("KP_EXACT_LOGS") ? atoi(getenv("KP_EXACT_LOGS")) : 0;
