@@ -499,6 +499,7 @@ def main():
     t0 = time.perf_counter()
     plan = engine.get_plan(prep["device"], gen_pat, a.max_block)
     prep["t_plan"] = time.perf_counter() - t0
+    plan.set_counts(prep["Mk"], prep["Uk"])  # first: the count width sets lanes_per_workgroup
     width = plan.info["lanes_per_workgroup"]
     cap = engine.pass_cap(groups, plan.lanes_that_fit(), width)
     # a step = one pass of the whole grid's CV plan on one GPU (engine.plan_passes: fold
@@ -513,7 +514,6 @@ def main():
     plan.reserve(most)  # the one large allocation of the run: the widest pass any modelled rank runs
     prep["t_alloc"] = time.perf_counter() - t0
     prep["alloc_lanes"] = most
-    plan.set_counts(prep["Mk"], prep["Uk"])
 
     def step(s):
         plan.run(step_passes[(s * world + rank) % len(step_passes)])

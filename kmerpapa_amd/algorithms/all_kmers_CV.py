@@ -38,7 +38,11 @@ def all_kmers(gen_pat, contextD, alphas, args, nmut, nunmut, index_mut=0):
     train_loss = {a_i: [] for a_i in range(len(alphas))}
     if index_mut != 0:
         contextD = {k: (v[index_mut], v[-1]) for k, v in contextD.items()}
-    dev = engine.get_device(engine.visible_devices()[0])  # no CPU path: raises without the library / a GPU
+    devices = engine.visible_devices()  # no CPU path: raises without the library / a GPU
+    if not devices:
+        raise engine.KPError(-3, "--score all_kmers runs on the GPU: no GPU is visible to the HIP runtime "
+                                 f"({engine.LIB_PATH})")
+    dev = engine.get_device(devices[0])
     prng = np.random.RandomState(args.seed)
     for _ in range(nit):
         make_all_folds_contextD_kmers(contextD, U_mem, M_mem, gen_pat, prng)

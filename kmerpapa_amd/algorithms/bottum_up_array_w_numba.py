@@ -31,6 +31,7 @@ def fit_partition(gen_pat, contextD, alpha, beta, penalty, itype, index_mut=0, d
     dev = engine.visible_devices()[0] if device is None else device
     plan = engine.get_plan(dev, gen_pat, max_block)
     plan.set_counts(Mk, Uk)
+    plan.require_lanes(1)  # a clean KPError (KP_E_NOMEM) if one lane does not fit the GPU
     rt, _, _ = plan.run([(-1, alpha, beta, [penalty])])
     leaves = plan.leaves(0)
     Mroot = itype(Mk.sum(dtype=np.uint64))

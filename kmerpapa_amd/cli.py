@@ -131,7 +131,7 @@ def write_partition(out, names, counts, contextD, alpha, beta, long_output):
             for i in range(len(pid)):
                 cn, cp = int(rows.U[i]), int(rows.M[i])
                 ctx = letters[i].tobytes().decode("ascii")
-                out.write(f"{ctx} {cn} {cp} {cp / (cp + cn)}{tails[int(pid[i])]}")
+                out.write(f"{ctx} {cn} {cp} {float(cp) / (cp + cn)}{tails[int(pid[i])]}")
             raise
         out.flush()
         if hasattr(out, "buffer"):
@@ -147,7 +147,20 @@ def write_partition(out, names, counts, contextD, alpha, beta, long_output):
 
 
 def main(args=None):
-    """Run the program (cli.py:118-318).  Returns an exit code."""
+    """Run the program (cli.py:118-318).  Returns an exit code: 0 as the reference's, 1
+    with a message on stderr when the lattice does not fit the GPU's memory (the
+    reference's numpy allocation would fail there, CV :93-102)."""
+    from .engine import KPError
+    try:
+        return _main(args)
+    except KPError as e:
+        if e.code != -2:  # KP_E_NOMEM
+            raise
+        print(f"kmerpapa: {e}", file=sys.stderr)
+        return 1
+
+
+def _main(args=None):
     clock = _Phases()
     parser = get_parser()
     args = parser.parse_args(args=args)

@@ -622,13 +622,24 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
         }
         const char *e = getenv("KP_HPD");
         if ((!e || atoi(e) != 0) && most >= 1 && most <= 64 && g.nblocks < (1ull << 29)) {
-            p->hps = most;
-            KP_HIP(dmalloc(&p->d_hpd, g.nblocks * most * sizeof(uint64_t)));
-            const unsigned nb = (unsigned)std::min<uint64_t>((g.nblocks + 255) / 256, 16384);
-            hipLaunchKernelGGL(kp_hpd_kernel, dim3(nb), dim3(256), 0, ctx->stream, g, p->d_tabs, p->d_hdig,
-                               (uint64_t)g.nblocks, most, p->d_hpd);
-            KP_HIP(hipGetLastError());
-            KP_HIP(hipStreamSynchronize(ctx->stream));
+            // optional: if it cannot be set up (e.g. out of memory) the plan keeps the
+            // hdig/tabs setup instead of failing
+            hipError_t he = dmalloc(&p->d_hpd, g.nblocks * most * sizeof(uint64_t));
+            if (he == hipSuccess) {
+                const unsigned nb = (unsigned)std::min<uint64_t>((g.nblocks + 255) / 256, 16384);
+                hipLaunchKernelGGL(kp_hpd_kernel, dim3(nb), dim3(256), 0, ctx->stream, g, p->d_tabs, p->d_hdig,
+                                   (uint64_t)g.nblocks, most, p->d_hpd);
+                he = hipGetLastError();
+                if (he == hipSuccess) he = hipStreamSynchronize(ctx->stream);
+            }
+            if (he == hipSuccess) {
+                p->hps = most;
+            } else {
+                (void)hipGetLastError();  // clear a sticky launch / allocation error
+                dfree(p->d_hpd);
+                p->d_hpd = nullptr;
+                p->hps = 0;
+            }
         }
     }
     *out = p;

@@ -524,6 +524,22 @@ class Plan:
         held = self.lanes_held * per
         return max(0, int((fr + held - reserve) // per))
 
+    def require_lanes(self, n=1, reserve=2 << 30):
+        """Lanes that fit device memory now (``lanes_that_fit``); raises :class:`KPError`
+        (KP_E_NOMEM) naming the lattice, its bytes per lane and the GPU's free memory if
+        not even ``n`` do -- the reference would allocate its ``[npat, nf]`` arrays anyway
+        (CV :93-102) and fail in numpy; a pass of zero lanes is never planned."""
+        fit = self.lanes_that_fit(reserve)
+        if fit < n:
+            fr, tot = self.device.mem()
+            per = self.info["bytes_per_lane"]
+            raise KPError(-2, f"the lattice of {self.gen_pat} ({self.info['npat']:,} cells) needs "
+                              f"{per / 1e9:.4g} GB of device memory per lane (float32 score per cell), "
+                              f"{n} lane(s) at least; GPU {self.device.device} has {(fr + self.lanes_held * per) / 1e9:.4g} "
+                              f"of {tot / 1e9:.4g} GB free after the plan's tables. Restrict the general pattern "
+                              f"with --super_pattern.")
+        return fit
+
     def close(self):
         if self._h:
             load().kp_plan_destroy(self._h)
@@ -826,18 +842,25 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0):
     this while the host draws the fold split (CV_tools.fold_tables drops the GIL)."""
     devices = list(devices if devices is not None else visible_devices()[:1])
 
+    errors = []
+
     def prep(dev, rep, chunk):
-        if chunk:
-            plan = get_plan(dev, gen_pat, max_block, replica=rep)
-            width = plan.info["lanes_per_workgroup"]
-            passes, _ = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit(), width), width)
-            plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
+        try:
+            if chunk:
+                plan = get_plan(dev, gen_pat, max_block, replica=rep)
+                width = plan.info["lanes_per_workgroup"]
+                passes, _ = plan_passes(chunk, pass_cap(chunk, plan.require_lanes(), width), width)
+                plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
+        except Exception as e:  # re-raised in the caller's thread
+            errors.append(e)
     threads = [threading.Thread(target=prep, args=(dev, rep, chunk))
                for dev, rep, chunk in zip(devices, _replicas(devices), _device_shares(groups, devices))]
     for th in threads:
         th.start()
     for th in threads:
         th.join()
+    if errors:
+        raise errors[0]
 
 
 PASS_LOG = None  # a list to receive one timing record per pass of run_groups (bench.py)
@@ -877,7 +900,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
                     plan.set_counts(M, U)
                 # passes in fold order (folds arrive in order), small groups beside a full one
                 width = plan.info["lanes_per_workgroup"]
-                passes, order = plan_passes(chunk, pass_cap(chunk, plan.lanes_that_fit(), width), width)
+                passes, order = plan_passes(chunk, pass_cap(chunk, plan.require_lanes(), width), width)
                 plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))  # one allocation
                 outs = []
                 queued = {}

@@ -112,6 +112,9 @@ class EmuPlan:
     def lanes_that_fit(self):
         return self.fit
 
+    def require_lanes(self, n=1):
+        return self.lanes_that_fit()
+
     def reserve(self, lanes):
         self.reserved = max(self.reserved, int(lanes))
 

@@ -235,56 +235,103 @@ def _leaf_kmers(gen_pat, leaves):
     return leaf, kidx
 
 
+def _tree_check_pass(plan, lat, groups, Mk, Uk, rt, re, nl):
+    """Every lane of the pass just run (``groups``, lanes group-major): the host walks the
+    lane's optimal tree top-down from the GPU's stored train scores (oracle/treecheck.py:
+    split candidates in the reference's scan order with the first minimum winning, the
+    single-pattern term from the host C library's log in CV :56-78's operation order, the
+    k-mer terms of CV :15-20) and requires every node's stored score to be the re-derived
+    one bit for bit; the root's train and test values returned by the pass must equal the
+    re-derived root (test = the float32 sums test[c1] + test[c2] along the tree, CV :47,
+    :158-163) and kp_fit_leaves the re-derived leaves in backtrack order.  The leaves
+    must also cover every k-mer exactly once.  Returns the number of tree nodes checked."""
+    from oracle import treecheck as T
+    Mall, Uall = Mk.sum(axis=1), Uk.sum(axis=1)
+    lane, nodes = 0, 0
+    for fold, a, b, pens in groups:
+        mte, ute = Mk[:, fold], Uk[:, fold]
+        for c in pens:
+            r = T.rederive(lat, lambda cells, j=lane: plan.gather_cells(j, cells), Mall - mte, Uall - ute,
+                           mte, ute, a, float(b), c)
+            where = (fold, a, c)
+            assert r["root_train"].view(np.uint32) == np.float32(rt[lane]).view(np.uint32), where
+            assert r["root_test"].view(np.uint32) == np.float32(re[lane]).view(np.uint32), where
+            leaves = plan.leaves(lane)
+            assert leaves.size == int(nl[lane]) and np.array_equal(leaves, r["leaves"]), where
+            _, kidx = _leaf_kmers(lat.gp, leaves)
+            assert kidx.size == lat.n_kmers and (np.bincount(kidx, minlength=lat.n_kmers) == 1).all(), where
+            nodes += r["nodes"]
+            lane += 1
+    return nodes
+
+
 @pytest.mark.timeout(1200)
-def test_9mer_full_cv_all_125_lanes_leaf_sums(cv_split):
-    """The whole 5x5x5 headline grid (25 passes of 5 lanes over 7.69e9 cells): for every
-    lane, the optimal partition (kp_fit_leaves) covers each k-mer exactly once, the root
-    train value equals the float64 sum of the leaves' single-pattern train terms and the
-    root test value the float64 sum of their test terms (CV :60-78, :158-163), both within
-    the float32 summation error of a tree of at most max_level + 1 levels."""
+def test_9mer_full_cv_all_125_lanes_tree_rederived(cv_split):
+    """The whole 5x5x5 headline grid (25 passes of 5 lanes over 7.69e9 cells): every lane's
+    root train and root test -- the numbers that reach the CVfile -- pinned bit for bit by
+    re-deriving the lane's whole optimal tree on the host from the GPU's stored scores
+    (_tree_check_pass)."""
     from kmerpapa_amd import engine
     from kmerpapa_amd.score_utils import get_betas
+    from oracle import treecheck as T
     sp = cv_split
     alphas, pens, nf = [0.5, 1.0, 2.0, 5.0, 10.0], [3.0, 4.0, 5.0, 6.0, 7.0], 5
     plan = engine.get_plan(engine.visible_devices()[0], GEN_PAT, 0)
     plan.set_counts(sp["Mk"], sp["Uk"])
-    nk = plan.info["n_kmers"]
+    lat = T.Lattice(GEN_PAT)
+    assert lat.n_kmers == plan.info["n_kmers"]
     Mk = sp["Mk"].astype(np.int64)
     Uk = sp["Uk"].astype(np.int64)
-    Mall, Uall = Mk.sum(axis=1), Uk.sum(axis=1)
-    tol = (plan.info["max_level"] + 2) * 2.0 ** -24
-    checked = 0
+    lanes = nodes = 0
     for a in alphas:
         betas = get_betas(a, sp["mtr"], sp["utr"])
         for f in range(nf):
-            beta = float(betas[f])
-            rt, re, nl = plan.run([(f, a, beta, pens)])
-            mte_k, ute_k = Mk[:, f], Uk[:, f]
-            mtr_k, utr_k = Mall - mte_k, Uall - ute_k
-            for j, c in enumerate(pens):
-                leaves = plan.leaves(j)
-                assert leaves.size == int(nl[j])
-                leaf, kidx = _leaf_kmers(GEN_PAT, leaves)
-                assert kidx.size == nk and (np.bincount(kidx, minlength=nk) == 1).all(), (a, f, c)
-                n = leaves.size
-                sums = [np.bincount(leaf, weights=v[kidx].astype(np.float64), minlength=n)
-                        for v in (mtr_k, utr_k, mte_k, ute_k)]
-                mtr, utr, mte, ute = sums
-                single = np.bincount(leaf, minlength=n) == 1
-                p = (mtr + a) / (((mtr + utr) + a) + beta)
-                lp, l1p = np.log(p), np.log(1.0 - p)
-                with np.errstate(invalid="ignore", divide="ignore"):
-                    tr_wide = c + np.where(mtr > 0, (-2.0 * mtr) * lp, 0.0) + np.where(utr > 0, (-2.0 * utr) * l1p, 0.0)
-                    te_wide = np.where(mte > 0, (-2.0 * mte) * lp, 0.0) + np.where(ute > 0, (-2.0 * ute) * l1p, 0.0)
-                    l1p_k = np.log1p(-p)
-                    tr_k = -2.0 * (np.where(mtr > 0, mtr * lp, 0.0) + np.where(utr > 0, utr * l1p_k, 0.0)) + c
-                    te_k = -2.0 * (np.where(mte > 0, mte * lp, 0.0) + np.where(ute > 0, ute * l1p_k, 0.0))
-                train = float(np.where(single, tr_k, tr_wide).sum())
-                test = float(np.where(single, te_k, te_wide).sum())
-                assert abs(float(rt[j]) - train) <= tol * abs(train), (a, f, c, float(rt[j]), train)
-                assert abs(float(re[j]) - test) <= tol * abs(test), (a, f, c, float(re[j]), test)
-                checked += 1
-    assert checked == 125
+            grp = [(f, a, float(betas[f]), pens)]
+            rt, re, nl = plan.run(grp)
+            nodes += _tree_check_pass(plan, lat, grp, Mk, Uk, rt, re, nl)
+            lanes += len(pens)
+    assert lanes == 125
+    print(f"9-mer grid: {lanes} lanes, {nodes} tree nodes re-derived")
+
+
+@pytest.mark.timeout(1500)
+def test_11mer_full_two_folds_all_lanes_tree_rederived():
+    """BASELINE configs[4] at full size (ANNNNMNNNNA, 7.69e9 cells, 10 folds, 7x7 grid):
+    folds 0 and 6, all 49 lanes each, run as the passes engine.plan_passes cuts the grid
+    into (5-lane fold pieces, five mixed two-alpha pieces and one 4-lane piece per fold):
+    every lane's root train, root test and partition pinned by the host tree re-derivation."""
+    from kmerpapa_amd import engine
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    from kmerpapa_amd.score_utils import get_betas
+    from oracle import treecheck as T
+    import bench
+    gp, nf = "ANNNNMNNNNA", 10
+    kmers, M, U = bench.synthetic_counts(gp, seed=9)
+    ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(1), np.uint32)
+    Mk, Uk = engine.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    ms, us = Mf.sum(axis=0, dtype=np.uint64), Uf.sum(axis=0, dtype=np.uint64)
+    grid = []
+    for a in ALPHAS11:
+        betas = get_betas(a, ms.sum() - ms, us.sum() - us)
+        grid += [(f, a, float(betas[f]), PENS11) for f in range(nf)]
+    engine.release_all()
+    plan = engine.get_plan(engine.visible_devices()[0], gp, 0)
+    plan.set_counts(Mk, Uk)
+    width = plan.info["lanes_per_workgroup"]
+    passes, _ = engine.plan_passes([g for g in grid if g[0] in (0, 6)], width, width)
+    assert sum(1 for p in passes if len({g[1] for g in p}) == 2) == 10  # mixed pieces
+    lat = T.Lattice(gp)
+    Mk, Uk = Mk.astype(np.int64), Uk.astype(np.int64)
+    lanes = nodes = 0
+    for pas in passes:
+        rt, re, nl = plan.run(pas)
+        nodes += _tree_check_pass(plan, lat, pas, Mk, Uk, rt, re, nl)
+        lanes += sum(len(g[3]) for g in pas)
+    assert lanes == 98
+    print(f"11-mer folds 0, 6: {lanes} lanes, {nodes} tree nodes re-derived")
+    engine.release_all()
 
 
 @pytest.mark.timeout(900)

@@ -58,6 +58,37 @@ def test_small_lattices_full_arrays(eng, case, max_block):
     plan.close()
 
 
+@pytest.mark.parametrize("max_block", [0, 16])
+def test_block_setup_without_pair_table(eng, monkeypatch, max_block):
+    """KP_HPD=0: the sweep's block setup from the packed digits and pair tables (the path
+    plans take when the per-plan pair table is off or cannot be built: blocks with more
+    than 64 high pairs, 2^29+ blocks, or no memory for it) -- config 2's 5-mer lattice,
+    5 folds x 2 penalties, every lane's full score array equals the oracle's."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    from kmerpapa_amd.score_utils import get_betas
+    from oracle import oracle as O
+    monkeypatch.setenv("KP_HPD", "0")
+    ctx, gp, nm, nu = context_table(5)
+    contexts, Mf, Uf = fold_tables(ctx, 5, np.random.RandomState(1), np.uint32)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    ms, us = Mf.sum(axis=0, dtype=np.uint64), Uf.sum(axis=0, dtype=np.uint64)
+    betas = get_betas(1.0, ms.sum() - ms, us.sum() - us)
+    plan = eng.Plan(eng.get_device(0), gp, max_block)
+    try:
+        assert plan.info["high_levels"] > 1
+        plan.set_counts(Mk, Uk)
+        pens = [3.0, 6.0]
+        plan.run([(f, 1.0, float(betas[f]), pens) for f in range(5)])
+        for j, c in enumerate(pens):
+            ref = O.cv_pass(gp, contexts, Mf, Uf, 1.0, betas, c, 32)
+            for f in range(5):
+                score, _ = plan.dump_lane(f * len(pens) + j)
+                assert bits_equal(score, ref["score"][:, f]), (max_block, c, f)
+    finally:
+        plan.close()
+
+
 @pytest.mark.parametrize("case", ["k3", "k4", "k3zero", "k3big"])
 def test_small_lattice_fits(eng, case):
     from kmerpapa_amd.algorithms import bottum_up_array_w_numba as fitm

@@ -119,6 +119,9 @@ def test_engine_run_groups_lane_granular_over_devices(monkeypatch):
         def lanes_that_fit(self):
             return 7
 
+        def require_lanes(self, n=1):
+            return self.lanes_that_fit()
+
         def reserve(self, lanes):
             assert lanes <= 7
 
@@ -235,6 +238,9 @@ def test_engine_run_groups_fold_feed_order(monkeypatch):
         def lanes_that_fit(self):
             return 5
 
+        def require_lanes(self, n=1):
+            return self.lanes_that_fit()
+
         def reserve(self, lanes):
             pass
 
@@ -290,6 +296,9 @@ def test_engine_run_groups_gpu_named_twice(monkeypatch):
 
         def lanes_that_fit(self):
             return 5
+
+        def require_lanes(self, n=1):
+            return self.lanes_that_fit()
 
         def reserve(self, lanes):
             pass
