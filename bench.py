@@ -384,7 +384,7 @@ def model_world(plan, prep, gen_pat, world, shadows):
             "wall_s_incl_alloc": max(x["wall_s"] + a for x, a in zip(shares, alloc)),
             "units": sum(x["units"] for x in shares),
             "share_kernel_ms": [round(x["kernel_ms"], 2) for x in shares],
-            "share_roofline_frac": [round(f, 4) for f in fracs],
+            "share_effective_roofline_frac": [round(f, 4) for f in fracs],
             "share_passes_start_s": [round(x["passes_start_s"], 4) for x in shares],
             "share_fold_split_s": [round(x["fold_split_s"], 4) for x in shares],
             "share_fold0_s": [x["fold_ready_s"][0] for x in shares],
@@ -427,20 +427,24 @@ def scaling_table(line, cv, prep, npat, world=1):
     one-time lane allocation) at every GPU count north_star names: N = 1 measured (the
     line's own step rate and roofline, the full CV run), N = 2, 4, 8 modelled (model_world:
     every rank's share run on this GPU beside N - 1 concurrent host sides).  units_per_s =
-    the whole grid's units (cells x folds x (alpha, c)) / CV wall-clock; roofline_frac = the
-    sweep kernels' compulsory bytes / their HIP-event time / 8 TB/s, per GPU (min and mean
-    over the ranks); weak_units_per_s = N x the measured per-GPU step rate (what the
+    the whole grid's units (cells x folds x (alpha, c)) / CV wall-clock; effective_roofline_frac
+    = the sweep kernels' compulsory (algorithmic) bytes / their HIP-event time / 8 TB/s, per
+    GPU (min and mean over the ranks; the measured line's also as roofline_frac, its PMC-based
+    headline fraction); weak_units_per_s = N x the measured per-GPU step rate (what the
     driver's scaling run measures).  Under torchrun (world > 1) the entry of N = world is the
     measured job itself (wall-clock max over ranks) and nothing is modelled."""
     total = npat * sum(len(g[3]) for g in prep["groups"])
     out = {str(world): {"units_per_s": total / cv["wall_s"], "units_per_s_incl_alloc": total / cv["wall_s_incl_alloc"],
-                 "roofline_frac": line["roofline"]["frac"], "roofline_frac_min": line["roofline"]["frac"],
+                 "effective_roofline_frac": line["roofline"]["effective_frac"],
+                 "effective_roofline_frac_min": line["roofline"]["effective_frac"],
+                 "roofline_frac": line["roofline"]["frac"],
                  "wall_s": cv["wall_s"], "wall_s_incl_alloc": cv["wall_s_incl_alloc"],
                  "hbm_alloc_s": cv["hbm_alloc_s"], "weak_units_per_s": line["value"], "measured": True}}
     for w, m in (cv.get("models") or {}).items():
-        fr = m["share_roofline_frac"]
+        fr = m["share_effective_roofline_frac"]
         out[w] = {"units_per_s": total / m["wall_s"], "units_per_s_incl_alloc": total / m["wall_s_incl_alloc"],
-                  "roofline_frac": sum(fr) / len(fr) if fr else None, "roofline_frac_min": min(fr) if fr else None,
+                  "effective_roofline_frac": sum(fr) / len(fr) if fr else None,
+                  "effective_roofline_frac_min": min(fr) if fr else None,
                   "wall_s": m["wall_s"], "wall_s_incl_alloc": m["wall_s_incl_alloc"],
                   "hbm_alloc_s": max(m["share_hbm_alloc_s"]), "speedup": m["speedup"],
                   "speedup_incl_alloc": m["speedup_incl_alloc"], "weak_units_per_s": int(w) * line["value"],
@@ -554,28 +558,35 @@ def main():
 
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
-        roof = {"bound": "hbm", "achieved": must / dp_s / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": must / dp_s / 1e9 / PEAK_HBM_GBS,
+        eff_gbs = must / dp_s / 1e9
+        roof = {"bound": "hbm", "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "traffic": (tr["hbm_bytes_per_pass"] if tr else None),
                 "kernel": "kp_dp_kernel (all launches of one pass)",
                 "kernel_ms_per_pass": dp_ms / a.steps, "launches_per_pass": launches / a.steps,
                 "avg_launch_ms": dp_ms / max(1, launches),
-                "bytes_per_unit": must / units_rank,
-                "basis": "achieved = ALGORITHMIC (effective) bandwidth, not a measured HBM rate: the bytes the "
-                         "blocked sweep must move per pass ((8 P_high + 4) B per unit: two child-row reads per "
-                         "high-position split pair + one score write; DESIGN.md 3) / HIP-event time of the pass's "
-                         "kp_dp_kernel launches; part of those bytes are Infinity-Cache hits, so the measured "
-                         "fabric figure is traffic_frac",
+                # effective (algorithmic) bandwidth: the bytes the blocked sweep must move
+                "effective_gbs": eff_gbs, "effective_frac": eff_gbs / PEAK_HBM_GBS,
+                "effective_bytes_per_unit": must / units_rank,
+                "effective_basis": "ALGORITHMIC bytes, not a measured HBM rate: (8 P_high + 4) B per unit (two "
+                                   "child-row reads per high-position split pair + one score write; DESIGN.md 3) / "
+                                   "HIP-event time of the pass's kp_dp_kernel launches; part of those bytes are "
+                                   "Infinity-Cache and L2 hits, so it can exceed what HBM delivers",
                 "floor_bytes_per_unit": 8.0, "floor_frac": floor / dp_s / 1e9 / PEAK_HBM_GBS,
                 "naive_equivalent_bytes_per_unit": naive / units_rank,
                 "naive_equivalent_gbs": naive / dp_s / 1e9}
         if tr:
-            roof["traffic_basis"] = ("L2-miss fabric traffic per pass: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE over "
-                                     "the pass's kp_dp_kernel dispatches; includes Infinity-Cache hits (an upper "
-                                     "bound on HBM bytes)")
+            # the headline fraction: MEASURED fabric bytes (PMC) over the same kernel time
+            roof["achieved"] = tr["hbm_bytes_per_pass"] / (dp_s / a.steps) / 1e9
+            roof["frac"] = roof["achieved"] / PEAK_HBM_GBS
+            roof["frac_basis"] = ("fabric (L2-miss, includes Infinity-Cache hits) - upper bound on HBM: rocprofv3 "
+                                  "FETCH_SIZE x2 + WRITE_SIZE over the pass's kp_dp_kernel dispatches (committed "
+                                  "profile at this kernel_tag) / HIP-event kernel time of this run; no gfx950 "
+                                  "counter separates Infinity-Cache hits from DRAM reads (DESIGN.md 5)")
             roof["traffic_source"] = tr.get("source")
-            roof["traffic_gbs"] = tr["hbm_bytes_per_pass"] / (dp_s / a.steps) / 1e9
-            roof["traffic_frac"] = roof["traffic_gbs"] / PEAK_HBM_GBS
+        else:
+            roof["achieved"] = eff_gbs
+            roof["frac"] = eff_gbs / PEAK_HBM_GBS
+            roof["frac_basis"] = "effective (no PMC profile committed at this kernel_tag): see effective_basis"
         n_gpus = min(world, max(1, ndev))
         line = {
             "metric": "patterns scored/sec (lattice cells x folds x (alpha,c)), 9-mer 5-fold CV 5x5 grid"

@@ -111,16 +111,16 @@ def test_scaling_table_entries():
     prep = _prep()
     npat = 1000
     total = npat * 125
-    line = {"value": 5.0e9, "roofline": {"frac": 0.9}}
+    line = {"value": 5.0e9, "roofline": {"frac": 0.8, "effective_frac": 0.9}}
     cv = {"wall_s": 10.0, "wall_s_incl_alloc": 13.0, "hbm_alloc_s": 3.0,
-          "models": {"8": {"wall_s": 1.25, "wall_s_incl_alloc": 4.25, "share_roofline_frac": [0.9, 0.8],
+          "models": {"8": {"wall_s": 1.25, "wall_s_incl_alloc": 4.25, "share_effective_roofline_frac": [0.9, 0.8],
                            "share_hbm_alloc_s": [3.0] * 8, "speedup": 8.0, "speedup_incl_alloc": 13.0 / 4.25}}}
     t = bench.scaling_table(line, cv, prep, npat)
     assert sorted(t) == ["1", "8"]
     assert t["1"]["measured"] and not t["8"]["measured"]
     assert t["1"]["units_per_s"] == total / 10.0 and t["1"]["units_per_s_incl_alloc"] == total / 13.0
     assert t["8"]["units_per_s"] == total / 1.25 and t["8"]["wall_s_incl_alloc"] == 4.25
-    assert abs(t["8"]["roofline_frac"] - 0.85) < 1e-12 and t["8"]["roofline_frac_min"] == 0.8
+    assert abs(t["8"]["effective_roofline_frac"] - 0.85) < 1e-12 and t["8"]["effective_roofline_frac_min"] == 0.8
     assert t["8"]["weak_units_per_s"] == 8 * 5.0e9 and t["8"]["hbm_alloc_s"] == 3.0
     t4 = bench.scaling_table(line, {"wall_s": 2.5, "wall_s_incl_alloc": 5.5, "hbm_alloc_s": 3.0}, prep, npat, world=4)
     assert sorted(t4) == ["4"] and t4["4"]["measured"] and t4["4"]["units_per_s"] == total / 2.5
