@@ -105,15 +105,18 @@ struct kp_dp_params {
 // kp_fma_log (kp_libm.h: fdlibm's algorithm with the hardware reciprocal and FMAs, ~45
 // instructions against ocml's ~80 of double-double arithmetic): pass 1 lane 124.3 -> 111.1
 // ms, 4 lanes 317.9 -> 312.3, 5 lanes 380.3 -> 377.0.  The 2- and 3-lane builds (80 VGPRs at
-// 6 waves per SIMD) and the mixed-group builds (two rates, four logs per cell) keep the
-// device's own log (ocml): with kp_fma_log their spills grow (3 lanes 248 -> 284 ms, 2 lanes
-// 179 -> 206, mixed 2 + 3 lanes 404 -> 409; profiles/r04/experiments/fmalog_ab.txt).
+// 6 waves per SIMD) keep the device's own log (ocml): with kp_fma_log their spills grow (3
+// lanes 248 -> 284 ms, 2 lanes 179 -> 206; profiles/r04/experiments/fmalog_ab.txt).  The
+// mixed-group builds (two rates, four logs per cell) of 4+ lanes take kp_fma_log since the
+// split scan's half chunks (KP_CHUNK_SPLIT) freed their registers: 5-lane mixed 123 -> 126
+// VGPRs, no VGPR spill, SGPR spills 24 -> 18; pass 397 -> 382 ms, 2 + 2 lanes 353 -> 339
+// (profiles/r05/experiments/fmamix_ab.txt; before the half chunks: 404 -> 409).
 // -DKP_FAST_LOG: kp_fast_log (fdlibm, IEEE division) in every build (A/B only).
 #ifndef KP_FMA_LOG_MASK
 #define KP_FMA_LOG_MASK 0x1F2u  // NL = 1, 4, 5, 6, 7, 8
 #endif
 #ifndef KP_FMA_LOG_MIX
-#define KP_FMA_LOG_MIX 0  // 1: the mixed builds too (A/B)
+#define KP_FMA_LOG_MIX 1  // the mixed builds too (of the NL in the mask: 4-8 lanes); 0 = ocml there (A/B)
 #endif
 template <int NL, bool MIX>
 __device__ inline double kp_dlog(double x) {
