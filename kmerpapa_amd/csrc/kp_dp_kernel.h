@@ -250,13 +250,17 @@ __device__ inline void kp_gather_items(const kp_dp_params &P, const kp_hpair *hp
 #ifndef KP_SMALL_NL
 #define KP_SMALL_NL 3  // widest group built for KP_SMALL_WAVES (A/B knob)
 #endif
+#ifndef KP_ONE_WAVES
+#define KP_ONE_WAVES KP_SMALL_WAVES  // the 1-lane build's waves per SIMD (A/B knob)
+#endif
 // HZ: the build that handles k-mer cells (only high level 0's blocks hold them; their
 // xlogy / xlog1py terms call the C library's logs, kp_libm.h); launches of higher levels
 // may use the build without that code (kp_hip.hip launch_dp).  MIX: the build for launch
 // classes that hold mixed groups (kp_group_dev.nl2 > 0: a second (alpha, beta) set for the
 // group's last lanes, a second pair of logs per cell); other classes use MIX = false
 template <typename CT, int NL, bool HZ, bool MIX>
-__global__ void __launch_bounds__(KP_DP_MAX_THREADS) __attribute__((amdgpu_waves_per_eu(NL <= KP_SMALL_NL ? KP_SMALL_WAVES : 1)))
+__global__ void __launch_bounds__(KP_DP_MAX_THREADS)
+__attribute__((amdgpu_waves_per_eu(NL == 1 ? KP_ONE_WAVES : NL <= KP_SMALL_NL ? KP_SMALL_WAVES : 1)))
 kp_dp_kernel(kp_dp_params P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const kp_geom &g = P.g;

@@ -288,4 +288,6 @@ def test_11mer_full_lattice_properties(eng):
     assert (cover == 1).all()
     assert 50 < len(names) < n_kmers
     assert abs(float(score) - total) <= 2e-6 * abs(total)
+    from tests.test_gpu_fullsize import _fit_tree_rederived
+    _fit_tree_rederived(gp, kmers, M, U, alpha, beta, pen, score, names)  # root + partition bit for bit
     eng.release_all()

@@ -11,6 +11,11 @@ properties of the optimal partition and of the CV roots, checked on the GPU resu
   LL + c |P|).
 The backtrack itself re-derives every node's decision from the stored scores and
 fails with KP_E_PARITY unless each one reproduces its float32 score bit for bit.
+Independently of it, the HOST re-derives every optimal tree (oracle/treecheck.py: the
+reference's recurrence with the C library's logs) from the GPU's stored scores and pins,
+bit for bit, the fit's root and partition and the root train / test values of every lane
+of the 9-mer grid (125) and of two folds of the 11-mer grid (98): the numbers that reach
+the CVfile.  Every cell of embedded sub-lattices is compared with the oracle as well.
 """
 import math
 
@@ -48,6 +53,24 @@ def _wide_term(m, u, alpha, beta, pen):
     return s
 
 
+def _fit_tree_rederived(gen_pat, kmers, M, U, alpha, beta, pen, score, names):
+    """The fit's root score and its partition in backtrack order (Fit :17-24, :121), bit for
+    bit: the host re-derives the whole optimal tree from the GPU's stored scores of the fit
+    lane (oracle/treecheck.py: the reference's scan order, first minimum, the C library's
+    logs; test counts zero)."""
+    from kmerpapa_amd import engine
+    from oracle import treecheck as T
+    plan = engine.get_plan(engine.visible_devices()[0], gen_pat, 0)  # the plan the fit ran on
+    lat = T.Lattice(gen_pat)
+    assert np.array_equal(engine.kmer_order(gen_pat, kmers), np.arange(lat.n_kmers))  # k-mer index order
+    z = np.zeros(lat.n_kmers, np.int64)
+    r = T.rederive(lat, lambda cells: plan.gather_cells(0, cells), np.asarray(M, np.int64), np.asarray(U, np.int64),
+                   z, z, alpha, beta, pen)
+    assert r["root_train"].view(np.uint32) == np.float32(score).view(np.uint32)
+    assert [lat.pattern(c) for c in r["leaves"]] == list(names)
+    return r
+
+
 def test_9mer_full_fit_properties(counts):
     from kmerpapa_amd import engine
     from kmerpapa_amd.algorithms import bottum_up_array_w_numba as fitm
@@ -76,6 +99,7 @@ def test_9mer_full_fit_properties(counts):
     assert (cover == 1).all()
     assert 50 < len(names) < n_kmers
     assert abs(float(score) - total) <= 2e-6 * abs(total)
+    _fit_tree_rederived(GEN_PAT, kmers, M, U, alpha, beta, pen, score, names)
     one = _wide_term(nm, nu, alpha, beta, pen)
     every = sum(_leaf_term(int(m), int(u), alpha, beta, pen) for m, u in zip(M, U))
     assert float(score) <= one * (1 + 1e-6) and float(score) <= every * (1 + 1e-6)
