@@ -1255,9 +1255,14 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
                 if (*q == ',') ++q;
             }
         }
+        // (counted among the positions that have split pairs: a fixed base of the general
+        // pattern, radix 1, sits last in the block order but has no child rows -- the 11-mer
+        // super pattern ANNNNMNNNNA has one, which left it with two non-temporal positions)
+        std::vector<int> slow_order;
+        for (int q = (int)hp.perm.size() - 1; q >= 0; --q)
+            if (g.r[g.t + hp.perm[q]] > 1) slow_order.push_back(hp.perm[q]);
         for (int H = 0; H <= hp.hmax; ++H)
-            for (int q = 0; q < per[H] && q < (int)hp.perm.size(); ++q)
-                ntmask_h[H] |= 1u << hp.perm[hp.perm.size() - 1 - q];
+            for (int q = 0; q < per[H] && q < (int)slow_order.size(); ++q) ntmask_h[H] |= 1u << slow_order[q];
         P.ntmask = ntmask_h[0];
     }
     P.stamps = nullptr;
