@@ -349,3 +349,23 @@ def test_cv_driver_over_8_devices_with_emulator_plans(monkeypatch):
         folds = [max(f for f, _, _ in p) for p in plans[(d, 0)].passes]
         assert folds == sorted(folds)
         assert all(sum(n for _, _, n in p) <= plans[(d, 0)].reserved for p in plans[(d, 0)].passes)
+
+
+def test_prepare_groups_surfaces_plan_errors(monkeypatch):
+    """engine.prepare_groups (run beside the fold split by the CV driver) re-raises an error
+    from any device's preparation in the caller, e.g. the lattice not fitting one lane."""
+    from kmerpapa_amd import engine
+
+    class TooBig:
+        info = {"lanes_per_workgroup": 5}
+
+        def require_lanes(self, n=1):
+            raise engine.KPError(-2, "does not fit")
+
+        def reserve(self, lanes):
+            raise AssertionError("nothing may be reserved")
+    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0, replica=0: TooBig())
+    groups = [(f, 1.0, 1.0, [3.0, 4.0]) for f in range(4)]
+    with pytest.raises(engine.KPError) as e:
+        engine.prepare_groups("NNMNN", groups, devices=[0, 1])
+    assert e.value.code == -2
