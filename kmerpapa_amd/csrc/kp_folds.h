@@ -15,6 +15,12 @@
 #pragma once
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+#endif
+
+#include "kp_logdata.h"
 
 namespace kpf {
 
@@ -95,8 +101,87 @@ struct loggam_table {
     }
 };
 
-inline double loggam_sum4(int64_t k0, int64_t k1, int64_t k2, int64_t k3) {
+inline const loggam_table &loggam_tab() {
     static const loggam_table t;
+    return t;
+}
+
+#if !defined(__HIP_DEVICE_COMPILE__)
+// loggam_sum4 with the four arguments' large-argument work in one 4-wide AVX2 + FMA
+// register each: the same IEEE operations in the same order per lane (the polynomial's
+// multiplies and adds unfused, as loggam is compiled; the divisions), and the C library's
+// log restated (kp_libm.h kp_libm_log: glibc's __log_fma, its table path -- every argument
+// here is >= 8) with its FMAs, so every lane's bits equal the scalar path's.  The split's
+// critical path is this function: ~3 calls per colour, ~75 % of a fold's draw.
+// 4 lanes of loggam's large-argument path (x0 = k, every k >= 8): the same IEEE operations
+// in the same order per lane as the scalar loggam (the polynomial's multiplies and adds
+// unfused, the divisions) and the C library's log restated (kp_libm.h kp_libm_log: glibc's
+// __log_fma table path) with its FMAs, so each lane's bits equal the scalar path's
+__attribute__((target("avx2,fma"))) inline __m256d loggam_big4(const __m256d X0) {
+    static const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03, 7.936507936507937e-04,
+                                 -5.952380952380952e-04, 8.417508417508418e-04, -1.917526917526918e-03,
+                                 6.410256410256410e-03, -2.955065359477124e-02, 1.796443723688307e-01,
+                                 -1.39243221690590e+00};
+    static const double tab[256] = KP_LOG_TAB;
+    static const double A[5] = KP_LOG_POLY;
+    const __m256d inv = _mm256_div_pd(_mm256_set1_pd(1.0), X0);
+    const __m256d X2 = _mm256_mul_pd(inv, inv);
+    __m256d G = _mm256_set1_pd(a[9]);
+    for (int i = 8; i >= 0; --i) G = _mm256_add_pd(_mm256_mul_pd(G, X2), _mm256_set1_pd(a[i]));
+    const __m256i ix = _mm256_castpd_si256(X0);
+    const __m256i tmp = _mm256_sub_epi64(ix, _mm256_set1_epi64x(0x3fe6000000000000ll));
+    const __m256i idx = _mm256_slli_epi64(_mm256_and_si256(_mm256_srli_epi64(tmp, 45), _mm256_set1_epi64x(127)), 1);
+    const __m256i kk = _mm256_srli_epi64(tmp, 52);  // >= 2 for x0 >= 8: a logical shift is the arithmetic one
+    const __m256i iz = _mm256_sub_epi64(ix, _mm256_and_si256(tmp, _mm256_set1_epi64x((long long)0xfff0000000000000ull)));
+    const __m256d invc = _mm256_i64gather_pd(tab, idx, 8);
+    const __m256d logc = _mm256_i64gather_pd(tab + 1, idx, 8);
+    const __m256d two52 = _mm256_set1_pd(4503599627370496.0);  // (double)k = bits(2^52 + k) - 2^52, exact
+    const __m256d kd = _mm256_sub_pd(_mm256_castsi256_pd(_mm256_or_si256(kk, _mm256_castpd_si256(two52))), two52);
+    const __m256d z = _mm256_castsi256_pd(iz);
+    const __m256d r = _mm256_fmadd_pd(z, invc, _mm256_set1_pd(-1.0));
+    const __m256d w = _mm256_fmadd_pd(kd, _mm256_set1_pd(KP_LOG_LN2HI), logc);
+    const __m256d hi = _mm256_add_pd(r, w);
+    const __m256d lo = _mm256_fmadd_pd(kd, _mm256_set1_pd(KP_LOG_LN2LO), _mm256_add_pd(_mm256_sub_pd(w, hi), r));
+    const __m256d r2 = _mm256_mul_pd(r, r);
+    const __m256d t1 = _mm256_fmadd_pd(r, _mm256_set1_pd(A[2]), _mm256_set1_pd(A[1]));
+    const __m256d r3 = _mm256_mul_pd(r, r2);
+    const __m256d t2 = _mm256_fmadd_pd(r, _mm256_set1_pd(A[4]), _mm256_set1_pd(A[3]));
+    const __m256d lo2 = _mm256_fmadd_pd(r2, _mm256_set1_pd(A[0]), lo);
+    const __m256d poly = _mm256_fmadd_pd(t2, r2, t1);
+    const __m256d L = _mm256_add_pd(_mm256_fmadd_pd(r3, poly, lo2), hi);
+    // gl0 / x0 + 0.5 * lg2pi + (x0 - 0.5) * log(x0) - x0, left to right
+    __m256d R = _mm256_add_pd(_mm256_div_pd(G, X0), _mm256_set1_pd(0.5 * 1.8378770664093453e+00));
+    R = _mm256_add_pd(R, _mm256_mul_pd(_mm256_sub_pd(X0, _mm256_set1_pd(0.5)), L));
+    return _mm256_sub_pd(R, X0);
+}
+
+// two independent loggam_sum4 sums at once (HRUA's d10 and its first candidate's term: the
+// candidate needs only the random draws, not d10): two dependent chains side by side
+__attribute__((target("avx2,fma"))) inline void loggam_sum4x2_avx2(const int64_t (&k)[8], const bool (&big)[8],
+                                                                   double *s0, double *s1) {
+    alignas(32) double x0[8];
+    for (int j = 0; j < 8; ++j) x0[j] = big[j] ? (double)k[j] : 8.0;
+    const __m256d R0 = loggam_big4(_mm256_load_pd(x0));
+    const __m256d R1 = loggam_big4(_mm256_load_pd(x0 + 4));
+    alignas(32) double r[8];
+    _mm256_store_pd(r, R0);
+    _mm256_store_pd(r + 4, R1);
+    const loggam_table &t = loggam_tab();
+    for (int j = 0; j < 8; ++j)
+        if (!big[j]) r[j] = t.v[k[j]];
+    *s0 = ((r[0] + r[1]) + r[2]) + r[3];
+    *s1 = ((r[4] + r[5]) + r[6]) + r[7];
+}
+
+inline bool cpu_avx2_fma() {
+    static const bool ok = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma") && !getenv("KP_FOLDS_SCALAR");
+    return ok;
+}
+#endif
+
+inline double loggam_sum4(int64_t k0, int64_t k1, int64_t k2, int64_t k3) {
+    const loggam_table &t = loggam_tab();
+
     static const double a[10] = {8.333333333333333e-02, -2.777777777777778e-03, 7.936507936507937e-04,
                                  -5.952380952380952e-04, 8.417508417508418e-04, -1.917526917526918e-03,
                                  6.410256410256410e-03, -2.955065359477124e-02, 1.796443723688307e-01,
@@ -127,6 +212,29 @@ inline double loggam_sum4(int64_t k0, int64_t k1, int64_t k2, int64_t k3) {
     return ((r[0] + r[1]) + r[2]) + r[3];
 }
 
+// loggam_sum4 of two argument sets: *s0 = set 0 (a0..a3), *s1 = set 1 (b0..b3), each bit for
+// bit loggam_sum4's value; with AVX2 + FMA the two sets' large arguments run as two 4-lane
+// chains side by side
+inline void loggam_sum4_pair(int64_t a0, int64_t a1, int64_t a2, int64_t a3, int64_t b0, int64_t b1, int64_t b2,
+                             int64_t b3, double *s0, double *s1) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    if (cpu_avx2_fma()) {
+        const int64_t k[8] = {a0, a1, a2, a3, b0, b1, b2, b3};
+        bool big[8], ok = true;
+        for (int j = 0; j < 8; ++j) {
+            big[j] = !((uint64_t)(k[j] - 1) < (uint64_t)(loggam_table::N - 1));
+            ok &= !big[j] || k[j] >= 8;  // (k <= 0 takes loggam's own path)
+        }
+        if (ok) {
+            loggam_sum4x2_avx2(k, big, s0, s1);
+            return;
+        }
+    }
+#endif
+    *s0 = loggam_sum4(a0, a1, a2, a3);
+    *s1 = loggam_sum4(b0, b1, b2, b3);
+}
+
 inline int64_t hypergeometric_hyp(mt19937 &rng, int64_t good, int64_t bad, int64_t sample) {
     const int64_t d1 = bad + good - sample;
     const double d2 = (double)(bad < good ? bad : good);
@@ -155,7 +263,11 @@ inline int64_t hypergeometric_hrua(mt19937 &rng, int64_t good, int64_t bad, int6
     const double d7 = sqrt((double)(popsize - m) * sample * d4 * d5 / (popsize - 1) + 0.5);
     const double d8 = D1 * d7 + D2;
     const int64_t d9 = (int64_t)floor((double)(m + 1) * (mingoodbad + 1) / (popsize + 2));
-    const double d10 = loggam_sum4(d9 + 1, mingoodbad - d9 + 1, m - d9 + 1, maxgoodbad - m + d9 + 1);
+    // d10 = loggam_sum4(d9 + 1, mingoodbad - d9 + 1, m - d9 + 1, maxgoodbad - m + d9 + 1): the
+    // same value whenever it is computed, so it is computed together with the first candidate
+    // that needs it (two independent chains side by side: the loop's latency is loggam's)
+    double d10 = 0.0;
+    bool have_d10 = false;
     const double mm = (double)(m < mingoodbad ? m : mingoodbad) + 1.0, fl = floor(d6 + 16 * d7);
     const double d11 = mm < fl ? mm : fl;
     int64_t Z;
@@ -165,7 +277,17 @@ inline int64_t hypergeometric_hrua(mt19937 &rng, int64_t good, int64_t bad, int6
         const double W = d6 + d8 * (Y - 0.5) / X;
         if (W < 0.0 || W >= d11) continue;  // fast rejection
         Z = (int64_t)floor(W);
-        const double T = d10 - loggam_sum4(Z + 1, mingoodbad - Z + 1, m - Z + 1, maxgoodbad - m + Z + 1);
+        double T;
+        if (!have_d10) {
+            have_d10 = true;
+            double s1;
+            loggam_sum4_pair(d9 + 1, mingoodbad - d9 + 1, m - d9 + 1, maxgoodbad - m + d9 + 1, Z + 1,
+                             mingoodbad - Z + 1, m - Z + 1, maxgoodbad - m + Z + 1, &d10, &s1);
+            T = Z == d9 ? 0.0 : d10 - s1;
+        } else {
+            // (Z == d9: the same four arguments as d10, so the difference is exactly +0.0)
+            T = Z == d9 ? 0.0 : d10 - loggam_sum4(Z + 1, mingoodbad - Z + 1, m - Z + 1, maxgoodbad - m + Z + 1);
+        }
         if ((X * (4.0 - X) - 3.0) <= T) break;  // fast acceptance
         if (X * (X - T) >= 1) continue;         // fast rejection
         if (2.0 * log(X) <= T) break;           // accept

@@ -75,3 +75,28 @@ def test_fold_stream_matches_fold_tables(nf):
             assert Mf.dtype == itype and np.array_equal(Mf, M[:, f]) and np.array_equal(Uf, U[:, f])
         s1, s2 = p1.get_state(), p2.get_state()
         assert np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]
+
+
+def test_fold_split_vector_and_scalar_paths_agree():
+    """kp_folds.h evaluates HRUA's d10 and first candidate as two AVX2 + FMA chains when the
+    host has them (loggam_sum4_pair), else with the scalar loggam: both give numpy's draws.
+    Here: a 9-mer-sized split (131,072 k-mers' M and U colours, counts up to ~1e5, totals
+    ~2.7e9) in two processes, one forced scalar (KP_FOLDS_SCALAR=1): identical folds."""
+    import hashlib
+    import os
+    import subprocess
+    import sys
+    code = ("import numpy as np, hashlib; from kmerpapa_amd import engine; "
+            "r = np.random.RandomState(5); c = np.concatenate([r.poisson(0.5, 131072), r.poisson(2e4, 131072)]); "
+            "print(hashlib.sha1(engine.fold_split(c.astype(np.uint64), 5, np.random.RandomState(1)).tobytes()).hexdigest())")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for scalar in (False, True):
+        env = dict(os.environ)
+        env.pop("KP_FOLDS_SCALAR", None)
+        if scalar:
+            env["KP_FOLDS_SCALAR"] = "1"
+        outs.append(subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                                   check=True).stdout.strip())
+    assert outs[0] == outs[1] and len(outs[0]) == 40
+    assert hashlib.sha1(b"").hexdigest() not in outs
