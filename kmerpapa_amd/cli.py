@@ -56,7 +56,10 @@ def get_parser():
     p.add_argument("-l", "--long_output", action="store_true", help="Print all k-mers in output format.")
     p.add_argument("-s", "--super_pattern", type=str,
                    help="If a super-pattern is provided the program will only consider k-mers that match that "
-                        "pattern.")
+                        "pattern. If for instance the \"--positive\" file contain all 5-mers at A->T mutated sites "
+                        "but the \"--background\" file contains 5-mers from all sites in the genome. Then "
+                        "\"--super_pattern NNANN\" should be specified to ignore 5-mers where A->T mutations cannot "
+                        "happen.")
     p.add_argument("--score", type=str, default="penalty_and_pseudo",
                    choices=["penalty_and_pseudo", "all_kmers", "BIC", "AIC", "HQ", "LL"],
                    help='Type of score function. Default is "penalty_and_pseudo". '
