@@ -649,23 +649,24 @@ def materialize(M, U, groups):
 
 
 # lanes a pass may hold when it packs groups of different widths (KMERPAPA_PASS_LANES; 0 =
-# one sweep workgroup's width, Plan.info["lanes_per_workgroup"])
+# one sweep workgroup's width + 1, Plan.info["lanes_per_workgroup"] + 1)
 PASS_LANES = int(os.environ.get("KMERPAPA_PASS_LANES", "0"))
 
 
 def pass_cap(groups, fit, width=0):
-    """Lanes per pass: PASS_LANES, by default one workgroup's ``width`` (5 at 9-mers), or
-    the largest group if wider, if that fits.  Packing a small piece beside a full one
-    saves one pass's fixed work (9-mer 5+1 lanes: 504 ms against 380 + 134), but every
-    lane of the widest pass is allocated for the whole job (30.8 GB per lane at 9-mers),
-    and an allocation that does not fit the HBM the driver has finished wiping waits for
-    the whole wipe of what earlier processes freed (~36 GB/s; 5.6 s after a 200 GB
-    process, tools/alloc_seq.sh): the smaller reservation is the likelier to fit, which is
-    worth more than the 10 ms the packing saves, so passes stay one workgroup wide
-    (DESIGN.md 6).  Two 5-lane groups never share a pass either: they are not faster per
-    lane."""
+    """Lanes per pass: PASS_LANES, by default one workgroup's ``width`` + 1 (6 at 9-mers),
+    or the largest group if wider, if that fits.  A pass of two device groups runs their
+    workgroups side by side in the same launches, so packing a small piece beside a full
+    one saves the small pass's fixed work: 9-mer 5 + 1 lanes 468 ms against 371 + 108, 4 + 2
+    482 against 310 + 182, 3 + 3 473 against 2 x 242 (profiles/r05/experiments/
+    pack_lanes.txt) -- the pieces a lane-granular multi-GPU share is left with.  Wider packs
+    gain less (5 + 2: 549 against 553) and every lane of the widest pass is allocated for the
+    whole job (30.8 GB per lane at 9-mers), so one extra lane is the default.  The
+    allocation's cost is the driver's wipe of HBM that earlier processes freed:
+    about as long for 154 as for 185 GB when HBM is still being wiped, ~1 ms for either when
+    it is clean.  Two 5-lane groups never share a pass: they are not faster per lane."""
     widest = max([len(g[3]) for g in groups] or [1])
-    cap = PASS_LANES or width or 7
+    cap = PASS_LANES or ((width + 1) if width else 7)
     return min(fit, max(cap, widest))
 
 

@@ -38,23 +38,26 @@ def test_cv_shares_cover_every_lane_once():
         assert max(lanes) - min(lanes) <= 1
 
 
-def test_pass_cap_is_one_workgroup_wide_by_default():
-    """Passes hold one workgroup's lanes (the job allocates its widest pass's lanes, and
-    HBM a process used before is wiped on allocation: an extra lane costs more than the
-    packing saves); a wider user group keeps its width; KMERPAPA_PASS_LANES
-    overrides."""
+def test_pass_cap_is_one_workgroup_plus_one_lane_by_default():
+    """Passes hold one workgroup's lanes plus one (a small piece of a split group packs
+    beside a full one: 5 + 1, 4 + 2, 3 + 3 lanes each save ~11 ms); a wider user
+    group keeps its width; KMERPAPA_PASS_LANES overrides."""
     groups = [(0, 1.0, 1.0, [1.0] * 5), (1, 1.0, 1.0, [1.0] * 3)]
     assert engine.PASS_LANES == 0
-    assert engine.pass_cap(groups, 9, 5) == 5
+    assert engine.pass_cap(groups, 9, 5) == 6
     assert engine.pass_cap(groups, 9) == 7  # (no width known: the old 7-lane packing)
     assert engine.pass_cap(groups, 4, 5) == 4
     assert engine.pass_cap([(0, 1.0, 1.0, [1.0] * 8)], 9, 5) == 8
-    # an 8-rank share of the 5x5x5 grid: [5, 5, 5, 1] -> passes [5], [5], [5], [1]
+    # an 8-rank share of the 5x5x5 grid: [5, 5, 5, 1] -> passes [5], [5], [5, 1]
     share = [(f, 1.0, 1.0, [1.0] * n) for f, n in enumerate([5, 5, 5, 1])]
     assert [[len(g[3]) for g in p] for p in engine.pack_passes(share, engine.pass_cap(share, 9, 5))] == \
-        [[5], [5], [5], [1]]
-    assert [[len(g[3]) for g in p] for p in engine.pack_passes(share, engine.pass_cap(share, 9))] == \
         [[5], [5], [5, 1]]
+    # two full groups never share a pass; 4 + 2 and 3 + 3 do
+    assert [[len(g[3]) for g in p] for p in engine.pack_passes(
+        [(f, 1.0, 1.0, [1.0] * n) for f, n in enumerate([5, 5, 4, 2, 3, 3])], 6)] == [[5], [5], [4, 2], [3, 3]]
+    # the 5x5x5 grid on one GPU: 25 passes of one group each
+    p9, _ = engine.plan_passes(_prep()["groups"], engine.pass_cap(_prep()["groups"], 9, 5), 5)
+    assert len(p9) == 25 and all(len(p) == 1 for p in p9)
 
 
 def test_plan_passes_fold_order_and_lane_mapping():
