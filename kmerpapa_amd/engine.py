@@ -874,8 +874,9 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     :class:`FoldFeed` (``U`` unused): then every GPU uploads the all-data counts first and
     each fold as it arrives, and runs its passes in fold order, so the first passes start
     before the last folds are drawn.  The lanes (one penalty of one group, group-major)
-    are cut into one contiguous, equal run per GPU and regrouped by (fold, alpha)
-    (``shard.rank_groups``, the same lane-granular split the ranks of a torchrun job use),
+    are split over the GPUs in equal shares and regrouped by (fold, alpha)
+    (``shard.assign_lanes``: whole groups where each fits a workgroup, else contiguous lane
+    runs -- the same split the ranks of a torchrun job use),
     each GPU's share packed into memory-sized passes, one host thread per GPU.  Returns
     ``(root_train, root_test, n_leaves)`` arrays over all lanes, group-major.
     """
@@ -884,7 +885,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     if not devices:
         raise KPError(-3, "no GPU visible")
     nd = len(devices)
-    shares = _device_shares(groups, devices)  # slots in order = lanes in order
+    shares = _device_shares(groups, devices)  # (results go back to lane order by shard.unshard)
     results = [None] * nd
     errors = []
 
@@ -963,7 +964,8 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
         th.join()
     if errors:
         raise errors[0]
-    return tuple(np.concatenate([r[i] for r in results]) for i in range(3))
+    from .shard import unshard
+    return tuple(unshard(groups, nd, [r[i] for r in results]) for i in range(3))
 
 
 run_groups.prepare = prepare_groups

@@ -11,15 +11,46 @@ from kmerpapa_amd import shard
 from tests.fixtures import golden_json
 
 
-def test_rank_groups_split_lanes_evenly_in_order():
-    groups = [(f, a, 0.1 * f + a, [3.0, 4.0, 5.0, 6.0, 7.0]) for a in (0.5, 1.0, 2.0, 5.0, 10.0) for f in range(5)]
-    flat = [(g[0], g[1], c) for g in groups for c in g[3]]
-    for world in (1, 2, 3, 4, 8):
-        parts = [shard.rank_groups(groups, r, world) for r in range(world)]
-        got = [(g[0], g[1], c) for p in parts for g in p for c in g[3]]
-        assert got == flat
-        sizes = [sum(len(g[3]) for g in p) for p in parts]
-        assert max(sizes) - min(sizes) <= 1
+def test_rank_groups_cover_every_lane_once_balanced():
+    """Every lane in exactly one rank's share, shares within one lane of each other, and
+    unshard puts the ranks' results back in the original lane order."""
+    g55 = [(f, a, 0.1 * f + a, [3.0, 4.0, 5.0, 6.0, 7.0]) for a in (0.5, 1.0, 2.0, 5.0, 10.0) for f in shard.fold_order(5)]
+    g77 = [(f, a, 0.1 * f + a, [2.0, 3.0, 4.0, 5.0, 6.0, 7.0, 8.0]) for a in (0.5, 1.0, 2.0) for f in shard.fold_order(10)]
+    gmix = [(f, 1.0, 1.0, [1.0] * (1 + f % 3)) for f in range(7)]
+    for groups in (g55, g77, gmix):
+        flat = [(g[0], g[1], c) for g in groups for c in g[3]]
+        for world in (1, 2, 3, 4, 8):
+            parts = [shard.rank_groups(groups, r, world) for r in range(world)]
+            ids = [shard.rank_lane_ids(groups, r, world) for r in range(world)]
+            got = [(g[0], g[1], c) for p in parts for g in p for c in g[3]]
+            assert sorted(sum(ids, [])) == list(range(len(flat)))
+            assert [flat[i] for i in sum(ids, [])] == got  # each rank's lanes are its ids, in order
+            sizes = [sum(len(g[3]) for g in p) for p in parts]
+            assert max(sizes) - min(sizes) <= 1, (len(groups), world, sizes)
+            vals = [np.asarray(i, np.float64) for i in ids]  # a rank's results = its lanes' numbers
+            assert np.array_equal(shard.unshard(groups, world, vals), np.arange(len(flat), dtype=np.float64))
+
+
+def test_headline_grid_over_8_ranks_whole_groups():
+    """The 5x5x5 grid over 8 ranks: 3 whole (alpha, fold) groups per rank; the leftover group
+    is one of fold 4 (drawn last), cut into 1-lane pieces for ranks 0-4, which are the ranks
+    holding a fold-0 group (they start when fold 0 is drawn); every 16-lane share packs as
+    [5], [5], [5 + 1]."""
+    from kmerpapa_amd import engine
+    groups = [(f, a, 1.0, [3.0, 4.0, 5.0, 6.0, 7.0]) for a in (0.5, 1.0, 2.0, 5.0, 10.0) for f in shard.fold_order(5)]
+    for r in range(8):
+        mine = shard.rank_groups(groups, r, 8)
+        sizes = sorted(len(g[3]) for g in mine)
+        folds = {g[0] for g in mine}
+        if r < 5:
+            assert sizes == [1, 5, 5, 5] and 0 in folds
+            one = [g for g in mine if len(g[3]) == 1][0]
+            assert one[0] == 4
+            passes, _ = engine.plan_passes(mine, engine.pass_cap(mine, 9, 5), 5)
+            assert sorted(sum(len(g[3]) for g in p) for p in passes) == [5, 5, 6]
+            assert min(g[0] for g in passes[0]) == 0  # the first pass is a fold-0 group
+        else:
+            assert sizes == [5, 5, 5]
 
 
 def test_chunk_bounds_cover_every_group_once():
