@@ -753,6 +753,15 @@ def plan_passes(groups, max_lanes, width=None):
     if passes and len({x[0] for x in passes[0]}) > 1:
         lo = min(x[0] for x in passes[0])
         passes[:1] = [[x for x in passes[0] if x[0] == lo], [x for x in passes[0] if x[0] != lo]]
+    # within a pass the fold with the most lanes comes first (lanes 0..): a 1-lane piece laid
+    # out before a 5-lane one costs the pass 486 vs 468 ms at 9-mers
+    # (profiles/r05/experiments/pack_order.txt); the pieces of one fold stay adjacent, so
+    # the library can still cut them into mixed device groups
+    for i, pas in enumerate(passes):
+        per_fold = {}
+        for x in pas:
+            per_fold[x[0]] = per_fold.get(x[0], 0) + len(x[3])
+        passes[i] = sorted(pas, key=lambda x: (-per_fold[x[0]], x[0]))  # stable within a fold
     lane_order = np.array([lid for pas in passes for x in pas for lid in x[4]], dtype=np.int64)
     return [[tuple(x[:4]) for x in pas] for pas in passes], lane_order
 

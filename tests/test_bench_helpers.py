@@ -62,13 +62,14 @@ def test_pass_cap_is_one_workgroup_plus_one_lane_by_default():
 
 def test_plan_passes_fold_order_and_lane_mapping():
     """8-rank shares of the 5x5x5 grid: [f4: 2 lanes, f0: 5, f1: 5, f2: 4] runs as passes
-    [f0], [f1], [f4 + f2] and [f2: 1, f3: 5, f4: 5, f0: 5] as [f0], [f3 + f2], [f4]: the first
+    [f0], [f1], [f2 + f4] and [f2: 1, f3: 5, f4: 5, f0: 5] as [f0], [f3 + f2], [f4]: the first
     pass needs only fold 0 (drawn first), a small piece never delays a lower fold's pass,
-    and results map back to the share's lane order."""
+    the fold with the most lanes of a pass is laid out first, and results map back to the
+    share's lane order."""
     share = [(4, 1.0, 1.0, [1.0, 2.0]), (0, 2.0, 1.0, [1.0] * 5), (1, 2.0, 1.0, [1.0] * 5), (2, 2.0, 1.0, [1.0] * 4)]
     for width in (None, 5):  # 5-lane fold pieces leave this share's groups whole
         passes, order = engine.plan_passes(share, engine.pass_cap(share, 9), width)
-        assert [[(g[0], len(g[3])) for g in p] for p in passes] == [[(0, 5)], [(1, 5)], [(4, 2), (2, 4)]]
+        assert [[(g[0], len(g[3])) for g in p] for p in passes] == [[(0, 5)], [(1, 5)], [(2, 4), (4, 2)]]
         lane_ids = np.arange(16)  # lane ids in the share's own order
         run = lane_ids[order]  # what the passes return
         assert (engine.unpermute_lanes(order, run) == lane_ids).all()
@@ -81,6 +82,11 @@ def test_plan_passes_fold_order_and_lane_mapping():
     passes3, order3 = engine.plan_passes(share3, engine.pass_cap(share3, 9), 5)
     assert [[(g[0], len(g[3])) for g in p] for p in passes3] == [[(0, 1)], [(2, 4)], [(3, 5)], [(4, 5)]]
     assert sorted(order3.tolist()) == list(range(15)) and order3[0] == 14
+    # a 1-lane fold-4 piece packed with a 5-lane fold-3 group is laid out after it
+    share4 = [(0, 1.0, 1.0, [1.0] * 5), (3, 1.0, 1.0, [1.0] * 5), (4, 2.0, 1.0, [1.0])]
+    passes4, order4 = engine.plan_passes(share4, engine.pass_cap(share4, 9, 5), 5)
+    assert [[(g[0], len(g[3])) for g in p] for p in passes4] == [[(0, 5)], [(3, 5), (4, 1)]]
+    assert order4.tolist() == list(range(11))
 
 
 def test_fold_pieces_cut_wide_grids_into_workgroup_widths():
