@@ -103,6 +103,13 @@ int kp_plan_get_info(const kp_plan *plan, kp_plan_info *out);
 /* Host-only (no GPU): build the plan's tables on the host and report their info -- the
  * lattice size and device bytes per lane a job would need, before any device is touched. */
 int kp_plan_host(const char *gen_pat, uint32_t max_block, kp_plan_info *out);
+/* Checks of the block list (test hooks; no reference counterpart).  The device builds the
+ * plan's block list (blocks by high level) from a closed-form rank rule.
+ * kp_block_order_check, host-only: *mismatches = blocks whose closed-form slot differs from
+ * the host's block walk.  kp_plan_block_check: *mismatches = entries of the plan's device
+ * list that differ from the host walk. */
+int kp_block_order_check(const char *gen_pat, uint32_t max_block, uint64_t *mismatches);
+int kp_plan_block_check(kp_plan *plan, uint64_t *mismatches);
 
 /* Upload fold counts of every k-mer: M, U are [n_kmers][nf] arrays of itype_bytes (4 or
  * 8) unsigned integers, k-mers in KmerEnumeration order (position 0 fastest, nucleotide

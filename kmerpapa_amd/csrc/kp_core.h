@@ -219,6 +219,42 @@ __host__ __device__ inline int kp_high_level(const kp_geom &g, const kp_postab *
     return s;
 }
 
+// the block order of kp::build_plan (high positions perm[0] fastest) in closed form
+struct kp_blockgen {
+    int hs;                 // high level sums 0 .. hs - 1
+    int8_t perm[KP_MAXK];   // high positions, fastest first
+};
+
+// Slot of block h in the plan's block list (blocks by high level, each level in the
+// mixed-radix order of perm) from build_plan's rank table brank[kh][16][hs] and level
+// offsets hoff; *hd / *hn = the block's packed high digits (4 bits) and split-pair counts
+// (3 bits per high position).  nblocks < 2^32 (build_plan), so 32-bit divisions suffice.
+__host__ __device__ inline uint64_t kp_block_slot(const kp_geom &g, const kp_postab *tabs, const kp_blockgen &bg,
+                                                  const uint32_t *brank, const uint64_t *hoff, uint64_t h,
+                                                  uint64_t *hd, uint64_t *hn) {
+    uint32_t dig[KP_MAXK];
+    uint32_t s = 0;
+    uint64_t w = 0, n = 0;
+    for (int i = 0; i < g.kh; ++i) {
+        const uint32_t d = ((uint32_t)h / (uint32_t)g.hcg[i]) % g.r[g.t + i];
+        const kp_postab &T = tabs[g.t + i];
+        dig[i] = d;
+        s += T.lev[d];
+        w |= (uint64_t)d << (4 * i);
+        n |= (uint64_t)T.np[d] << (3 * i);
+    }
+    uint64_t rank = 0;
+    uint32_t above = 0;
+    for (int j = g.kh - 1; j >= 0; --j) {
+        const int i = bg.perm[j];
+        rank += brank[((uint32_t)j * 16u + dig[i]) * (uint32_t)bg.hs + (s - above)];
+        above += tabs[g.t + i].lev[dig[i]];
+    }
+    *hd = w;
+    *hn = n;
+    return hoff[s] + rank;
+}
+
 // is cell (h, l) a k-mer (every digit a nucleotide)?
 __host__ __device__ inline bool kp_is_kmer(const kp_geom &g, uint64_t h, uint32_t lowinfo) {
     for (int i = 0; i < g.t; ++i)

@@ -365,6 +365,33 @@ __global__ void kp_hpd_kernel(kp_geom g, const kp_postab *__restrict__ tabs, con
     }
 }
 
+// The block list (hlist / kpos / hdig / hnp) of kp::build_plan's block order, built on the
+// device from the plan's rank table instead of walked and uploaded by the host (2.3 M
+// blocks at 9-mers: the walk was most of the plan's start-up, before the first pass).  One
+// thread per block h; every slot is written once (kp_block_slot is a bijection).
+__global__ void kp_blocks_kernel(kp_geom g, const kp_postab *__restrict__ tabs, kp_blockgen bg,
+                                 const uint32_t *__restrict__ brank, const uint64_t *__restrict__ hoff,
+                                 uint32_t *__restrict__ hlist, uint32_t *__restrict__ kpos, uint64_t *__restrict__ hdig,
+                                 uint64_t *__restrict__ hnp) {
+    for (uint64_t h = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; h < g.nblocks;
+         h += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t hd, hn;
+        const uint64_t q = kp_block_slot(g, tabs, bg, brank, hoff, h, &hd, &hn);
+        hlist[q] = (uint32_t)h;
+        kpos[h] = (uint32_t)q;
+        hdig[q] = hd;
+        hnp[q] = hn;
+    }
+}
+
+static kp_blockgen blockgen_of(const kp::host_plan &hp) {
+    kp_blockgen bg;
+    memset(&bg, 0, sizeof(bg));
+    bg.hs = hp.hs;
+    for (int j = 0; j < hp.g.kh; ++j) bg.perm[j] = (int8_t)hp.perm[j];
+    return bg;
+}
+
 // the C library's log (fn 1) or log1p (fn 2) as restated for the device (kp_libm.h), the
 // device's own log (fn 0), the table-free fast log (fn 3, kp_fast_log) or its FMA form (fn 4, kp_fma_log)
 __global__ void kp_libm_kernel(const double *__restrict__ x, double *__restrict__ y, uint64_t n, int fn) {
@@ -589,12 +616,45 @@ void kp_destroy(kp_ctx *c) {
     delete c;
 }
 
+}  // extern "C"
+
+// The plan's block list built on the device (kp_blocks_kernel): rank table and level
+// offsets up, one launch, the small tables freed once it has run.
+static int device_blocks(kp_plan *p) {
+    const kp_geom &g = p->hp.g;
+    uint32_t *d_brank = nullptr;
+    uint64_t *d_hoff = nullptr;
+    int rc;
+    if ((rc = upload(&d_brank, p->hp.brank)) || (rc = upload(&d_hoff, p->hp.hoff))) {
+        dfree(d_brank);
+        dfree(d_hoff);
+        return rc;
+    }
+    hipError_t he = dmalloc(&p->d_hlist, g.nblocks * sizeof(uint32_t));
+    if (he == hipSuccess) he = dmalloc(&p->d_kpos, g.nblocks * sizeof(uint32_t));
+    if (he == hipSuccess) he = dmalloc(&p->d_hdig, g.nblocks * sizeof(uint64_t));
+    if (he == hipSuccess) he = dmalloc(&p->d_hnp, g.nblocks * sizeof(uint64_t));
+    if (he == hipSuccess) {
+        const unsigned nb = (unsigned)std::min<uint64_t>((g.nblocks + 255) / 256, 16384);
+        hipLaunchKernelGGL(kp_blocks_kernel, dim3(nb), dim3(256), 0, p->ctx->stream, g, p->d_tabs, blockgen_of(p->hp),
+                           d_brank, d_hoff, p->d_hlist, p->d_kpos, p->d_hdig, p->d_hnp);
+        he = hipGetLastError();
+        if (he == hipSuccess) he = hipStreamSynchronize(p->ctx->stream);
+    }
+    dfree(d_brank);
+    dfree(d_hoff);
+    if (he != hipSuccess) return fail(KP_E_HIP, std::string("block list: ") + hipGetErrorString(he));
+    return KP_OK;
+}
+
+extern "C" {
+
 int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan **out) {
     if (!ctx || !gen_pat || !out) return fail(KP_E_ARG, "null argument");
     KP_HIP(hipSetDevice(ctx->device));
     kp_plan *p = new kp_plan();
     p->ctx = ctx;
-    std::string err = kp::build_plan(gen_pat, max_block ? max_block : 4096u, p->hp);
+    std::string err = kp::build_plan(gen_pat, max_block ? max_block : 4096u, p->hp, false);
     if (!err.empty()) {
         delete p;
         return fail(KP_E_ARG, err);
@@ -602,10 +662,18 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
     int rc;
     if ((rc = upload(&p->d_tabs, p->hp.tabs)) || (rc = upload(&p->d_lowinfo, p->hp.lowinfo)) ||
         (rc = upload(&p->d_loff, p->hp.loff)) || (rc = upload(&p->d_klofs, p->hp.klofs)) ||
-        (rc = upload(&p->d_kllist, p->hp.kllist)) || (rc = upload(&p->d_hlist, p->hp.hlist)) || (rc = upload(&p->d_kpos, p->hp.kpos)) ||
-        (rc = upload(&p->d_ldesc, p->hp.ldesc)) ||
-        (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_hnp, p->hp.hnp)) || (rc = upload(&p->d_lowmask, p->hp.lowmask)) ||
-        (rc = upload(&p->d_lpairs, p->hp.lpairs))) {
+        (rc = upload(&p->d_kllist, p->hp.kllist)) || (rc = upload(&p->d_ldesc, p->hp.ldesc)) ||
+        (rc = upload(&p->d_lowmask, p->hp.lowmask)) || (rc = upload(&p->d_lpairs, p->hp.lpairs))) {
+        kp_plan_destroy(p);
+        return rc;
+    }
+    if (p->hp.blocks_on_host) {  // an experiment block order (KP_BLOCK_TILE / KP_BLOCK_ORDER)
+        if ((rc = upload(&p->d_hlist, p->hp.hlist)) || (rc = upload(&p->d_kpos, p->hp.kpos)) ||
+            (rc = upload(&p->d_hdig, p->hp.hdig)) || (rc = upload(&p->d_hnp, p->hp.hnp))) {
+            kp_plan_destroy(p);
+            return rc;
+        }
+    } else if ((rc = device_blocks(p))) {
         kp_plan_destroy(p);
         return rc;
     }
@@ -697,9 +765,65 @@ int kp_plan_get_info(const kp_plan *p, kp_plan_info *o) {
 int kp_plan_host(const char *gen_pat, uint32_t max_block, kp_plan_info *o) {
     if (!gen_pat || !o) return fail(KP_E_ARG, "null argument");
     kp::host_plan hp;
-    std::string err = kp::build_plan(gen_pat, max_block ? max_block : 4096u, hp);
+    std::string err = kp::build_plan(gen_pat, max_block ? max_block : 4096u, hp, false);
     if (!err.empty()) return fail(KP_E_ARG, err);
     info_of(hp, o);
+    return KP_OK;
+}
+
+// Host-only (no GPU): the closed-form block order (kp_block_slot) against build_plan's
+// block walk, every block of the lattice; *mismatches = blocks whose slot, digits or
+// split-pair counts differ.
+int kp_block_order_check(const char *gen_pat, uint32_t max_block, uint64_t *mismatches) {
+    if (!gen_pat || !mismatches) return fail(KP_E_ARG, "null argument");
+    kp::host_plan hp;
+    std::string err = kp::build_plan(gen_pat, max_block ? max_block : 4096u, hp, true);
+    if (!err.empty()) return fail(KP_E_ARG, err);
+    const kp_blockgen bg = blockgen_of(hp);
+    uint64_t bad = 0;
+    std::vector<uint8_t> seen(hp.g.nblocks, 0);
+    for (uint64_t h = 0; h < hp.g.nblocks; ++h) {
+        uint64_t hd, hn;
+        const uint64_t q = kp_block_slot(hp.g, hp.tabs.data(), bg, hp.brank.data(), hp.hoff.data(), h, &hd, &hn);
+        if (q >= hp.g.nblocks || seen[q] || hp.hlist[q] != h || hp.kpos[h] != q || hp.hdig[q] != hd || hp.hnp[q] != hn)
+            ++bad;
+        else
+            seen[q] = 1;
+    }
+    *mismatches = bad;
+    return KP_OK;
+}
+
+// The plan's device block list (kp_blocks_kernel, or the upload of an experiment order)
+// against build_plan's host walk; *mismatches = differing entries of hlist, kpos, hdig
+// and hnp together.
+int kp_plan_block_check(kp_plan *p, uint64_t *mismatches) {
+    if (!p || !mismatches) return fail(KP_E_ARG, "null argument");
+    KP_HIP(hipSetDevice(p->ctx->device));
+    kp::host_plan hp;
+    std::string err = kp::build_plan(p->hp.gp.c_str(), 0, hp, true);
+    if (!err.empty()) return fail(KP_E_ARG, err);
+    if (hp.g.nblocks != p->hp.g.nblocks || hp.g.B != p->hp.g.B) {  // built with another block budget
+        kp::host_plan h2;
+        for (uint32_t mb = 1; mb <= 65536u; mb *= 2) {
+            if (!kp::build_plan(p->hp.gp.c_str(), mb, h2, true).empty()) continue;
+            if (h2.g.B == p->hp.g.B) break;
+        }
+        if (h2.g.B != p->hp.g.B) return fail(KP_E_ARG, "cannot rebuild the plan's block size");
+        hp = std::move(h2);
+    }
+    const uint64_t n = hp.g.nblocks;
+    std::vector<uint32_t> hl(n), kp(n);
+    std::vector<uint64_t> hd(n), hn(n);
+    KP_HIP(hipStreamSynchronize(p->ctx->stream));
+    KP_HIP(hipMemcpy(hl.data(), p->d_hlist, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    KP_HIP(hipMemcpy(kp.data(), p->d_kpos, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    KP_HIP(hipMemcpy(hd.data(), p->d_hdig, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    KP_HIP(hipMemcpy(hn.data(), p->d_hnp, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    uint64_t bad = 0;
+    for (uint64_t q = 0; q < n; ++q)
+        bad += (hl[q] != hp.hlist[q]) + (kp[q] != hp.kpos[q]) + (hd[q] != hp.hdig[q]) + (hn[q] != hp.hnp[q]);
+    *mismatches = bad;
     return KP_OK;
 }
 

@@ -59,13 +59,18 @@ struct host_plan {
     std::vector<uint64_t> hnp;         // [nblocks] their split pairs per high position, 3 bits each
     std::vector<uint64_t> hoff;        // [hmax + 2]
     std::vector<int> perm;             // high positions of the block order, fastest first
+    int hs = 0;                        // high level sums 0 .. hs - 1
+    std::vector<uint32_t> brank;       // [kh][16][hs] rank table of the block order (build_plan)
+    bool blocks_on_host = true;        // hlist / kpos / hdig / hnp built here
     uint32_t kh_nuc_weight = 0;
     // algorithmic accounting: split pairs summed over all cells
     double pairs_total = 0.0, pairs_low = 0.0, pairs_high = 0.0;
 };
 
 // Build the plan.  max_block bounds the LDS block (cells); returns "" or an error text.
-inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan &P) {
+// block_tables = false leaves hlist / kpos / hdig / hnp to the device (kp_blocks_kernel,
+// from perm, brank and hoff) unless an experiment block order is set (blocks_on_host).
+inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan &P, bool block_tables = true) {
     P = host_plan();
     P.gp = gen_pat ? gen_pat : "";
     int k = (int)P.gp.size();
@@ -111,7 +116,12 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     g.t = t;
     g.kh = k - t;
     g.B = (uint32_t)(t < k ? g.cgl[t] : acc);
-    g.Bpad = (g.B + 16u) & ~15u;  // >= B + 1: slot B is the +inf cell of padded pair lists
+    {  // >= B + 1: slot B is the +inf cell of padded pair lists; a multiple of KP_BPAD_ALIGN floats
+        const char *e = getenv("KP_BPAD_ALIGN");
+        uint32_t al = e ? (uint32_t)atoi(e) : 16u;
+        if (al < 16u || (al & (al - 1u))) al = 16u;
+        g.Bpad = (g.B + al) & ~(al - 1u);
+    }
     g.nblocks = acc / g.B;
     uint32_t nkl = 1;
     for (int i = 0; i < t; ++i) nkl *= g.n[i];
@@ -275,141 +285,167 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     P.hoff.assign(hmax + 2, 0);
     if (g.nblocks > 0xFFFFFFFFull) return "too many blocks for 32-bit block ids";
     if (g.kh > 15) return "too many high positions for packed digits";
-    // high levels of every block: a mixed-radix counter over h (high position 0 fastest)
-    // keeps the digits and their level sum, no 64-bit divisions (this runs on the host
-    // beside the fold split, before the first pass can start)
-    std::vector<uint8_t> hl(g.nblocks);
-    {
-        std::vector<uint32_t> dig(g.kh, 0);
-        int s = 0;
-        for (uint64_t h = 0; h < g.nblocks; ++h) {
-            hl[h] = (uint8_t)s;
-            P.hoff[s + 1]++;
-            for (int i = 0; i < g.kh; ++i) {
-                const kp_postab &T = P.tabs[g.t + i];
-                s -= T.lev[dig[i]];
-                if (++dig[i] < g.r[g.t + i]) {
-                    s += T.lev[dig[i]];
-                    break;
-                }
-                dig[i] = 0;
-                s += T.lev[0];
-            }
+    // Block order inside a level = the order the sweep kernel runs them in, which sets how
+    // often a child row read by several parents is still in L2 / the Infinity Cache.
+    // Parents of one child differ in one high position, so the positions that vary fastest
+    // get their reuse: those with the most split pairs (largest radix) go first, later
+    // positions before earlier ones (measured: random order +25 % time, ascending h
+    // (position t fastest) +1 %, this order the best of those tried).
+    // KP_BLOCK_PERM="5-4-..." (high positions, fastest first) and KP_BLOCK_ORDER=1
+    // (shuffled) / KP_BLOCK_TILE=T override it for experiments.
+    std::vector<int> perm;
+    if (const char *pe = getenv("KP_BLOCK_PERM")) {  // digits separated by any non-digit
+        for (const char *c = pe; *c;) {
+            const int v = atoi(c);
+            if (v >= 0 && v < g.kh && std::find(perm.begin(), perm.end(), v) == perm.end()) perm.push_back(v);
+            while (*c >= '0' && *c <= '9') ++c;
+            while (*c && (*c < '0' || *c > '9')) ++c;
         }
+    } else {
+        for (int i = g.kh - 1; i >= 0; --i) perm.push_back(i);
+        std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return g.r[g.t + a] > g.r[g.t + b]; });
     }
-    for (int s = 0; s <= hmax; ++s) P.hoff[s + 1] += P.hoff[s];
-    P.hlist.resize(g.nblocks);
+    for (int i = g.kh - 1; i >= 0; --i)  // complete a partial explicit permutation
+        if (std::find(perm.begin(), perm.end(), i) == perm.end()) perm.push_back(i);
+    P.perm = perm;
+    // Rank tables: the blocks are numbered by a mixed-radix counter, perm[0] fastest; block
+    // n goes to hoff[s] + (the number of blocks before n with the same high level s).  With
+    // C_j(x) = the digit tuples of positions perm[0..j) whose levels sum to x, that count is
+    // the sum over j of brank[j][digit at perm[j]][s - levels of the positions above j],
+    // brank[j][d][y] = sum over d' < d of C_j(y - lev(d')) -- a closed form, so the device
+    // builds the block list itself (kp_blocks_kernel) and the host never walks the blocks.
+    const int HS = hmax + 1;
+    P.hs = HS;
     {
-        // Block order inside a level = the order the sweep kernel runs them in, which sets
-        // how often a child row read by several parents is still in L2 / the Infinity Cache.
-        // Parents of one child differ in one high position, so the positions that vary
-        // fastest get their reuse: those with the most split pairs (largest radix) go
-        // first, later positions before earlier ones (measured: random order +25 % time,
-        // ascending h (position t fastest) +1 %, this order the best of those tried;
-        // DESIGN.md §5).  KP_BLOCK_PERM="5-4-..." (high positions, fastest first) and
-        // KP_BLOCK_ORDER=1 (shuffled) override it for experiments.
-        std::vector<int> perm;
-        if (const char *pe = getenv("KP_BLOCK_PERM")) {  // digits separated by any non-digit
-            for (const char *c = pe; *c;) {
-                const int v = atoi(c);
-                if (v >= 0 && v < g.kh && std::find(perm.begin(), perm.end(), v) == perm.end()) perm.push_back(v);
-                while (*c >= '0' && *c <= '9') ++c;
-                while (*c && (*c < '0' || *c > '9')) ++c;
-            }
-        } else {
-            for (int i = g.kh - 1; i >= 0; --i) perm.push_back(i);
-            std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return g.r[g.t + a] > g.r[g.t + b]; });
+        std::vector<uint64_t> C((size_t)(g.kh + 1) * HS, 0);
+        C[0] = 1;
+        P.brank.assign((size_t)g.kh * 16 * HS, 0);
+        for (int j = 0; j < g.kh; ++j) {
+            const kp_postab &T = P.tabs[g.t + perm[j]];
+            const uint32_t r = g.r[g.t + perm[j]];
+            for (uint32_t d = 0; d < r; ++d)
+                for (int y = 0; y < HS; ++y) {
+                    const uint64_t c = y >= T.lev[d] ? C[(size_t)j * HS + y - T.lev[d]] : 0;
+                    if (d + 1 < 16) P.brank[((size_t)j * 16 + d + 1) * HS + y] = P.brank[((size_t)j * 16 + d) * HS + y] + (uint32_t)c;
+                    C[(size_t)(j + 1) * HS + y] += c;
+                }
         }
-        for (int i = g.kh - 1; i >= 0; --i)  // complete a partial explicit permutation
-            if (std::find(perm.begin(), perm.end(), i) == perm.end()) perm.push_back(i);
-        P.perm = perm;
-        std::vector<uint64_t> fill(P.hoff.begin(), P.hoff.end() - 1);
-        // KP_BLOCK_TILE=T (experiment): tiles of T digits per high position, the digits
-        // inside a tile (perm order) varying faster than the tile coordinates
-        const char *te = getenv("KP_BLOCK_TILE");
-        const uint32_t tile = te ? (uint32_t)atoi(te) : 0u;
-        if (tile > 0) {
-            std::vector<uint32_t> tr(g.kh), to(g.kh, 0), ti(g.kh, 0);
-            for (int i = 0; i < g.kh; ++i) tr[i] = (g.r[g.t + i] + tile - 1) / tile;
-            for (;;) {
-                std::fill(ti.begin(), ti.end(), 0u);
-                for (;;) {
-                    bool ok = true;
-                    uint64_t h = 0;
-                    for (int i = 0; i < g.kh; ++i) {
-                        const uint32_t d = to[i] * tile + ti[i];
-                        if (d >= g.r[g.t + i]) { ok = false; break; }
-                        h += (uint64_t)d * g.hcg[i];
+        for (int s = 0; s <= hmax; ++s) P.hoff[s + 1] = P.hoff[s] + C[(size_t)g.kh * HS + s];
+        if (P.hoff[hmax + 1] != g.nblocks) return "block level counts do not cover every block";
+    }
+    const char *te = getenv("KP_BLOCK_TILE");
+    const uint32_t tile = te ? (uint32_t)atoi(te) : 0u;
+    const char *bo = getenv("KP_BLOCK_ORDER");
+    const bool shuffled = bo && atoi(bo) == 1;
+    P.blocks_on_host = block_tables || tile > 0 || shuffled;
+    if (P.blocks_on_host) {
+        // high levels of every block: a mixed-radix counter over h (high position 0 fastest)
+        // keeps the digits and their level sum, no 64-bit divisions
+        std::vector<uint8_t> hl(g.nblocks);
+        {
+            std::vector<uint32_t> dig(g.kh, 0);
+            int s = 0;
+            for (uint64_t h = 0; h < g.nblocks; ++h) {
+                hl[h] = (uint8_t)s;
+                for (int i = 0; i < g.kh; ++i) {
+                    const kp_postab &T = P.tabs[g.t + i];
+                    s -= T.lev[dig[i]];
+                    if (++dig[i] < g.r[g.t + i]) {
+                        s += T.lev[dig[i]];
+                        break;
                     }
-                    if (ok) P.hlist[fill[hl[h]]++] = (uint32_t)h;
+                    dig[i] = 0;
+                    s += T.lev[0];
+                }
+            }
+        }
+        P.hlist.resize(g.nblocks);
+        {
+            std::vector<uint64_t> fill(P.hoff.begin(), P.hoff.end() - 1);
+            // KP_BLOCK_TILE=T (experiment): tiles of T digits per high position, the digits
+            // inside a tile (perm order) varying faster than the tile coordinates
+            if (tile > 0) {
+                std::vector<uint32_t> tr(g.kh), to(g.kh, 0), ti(g.kh, 0);
+                for (int i = 0; i < g.kh; ++i) tr[i] = (g.r[g.t + i] + tile - 1) / tile;
+                for (;;) {
+                    std::fill(ti.begin(), ti.end(), 0u);
+                    for (;;) {
+                        bool ok = true;
+                        uint64_t h = 0;
+                        for (int i = 0; i < g.kh; ++i) {
+                            const uint32_t d = to[i] * tile + ti[i];
+                            if (d >= g.r[g.t + i]) { ok = false; break; }
+                            h += (uint64_t)d * g.hcg[i];
+                        }
+                        if (ok) P.hlist[fill[hl[h]]++] = (uint32_t)h;
+                        int j = 0;
+                        for (; j < g.kh; ++j) {
+                            const int i = perm[j];
+                            if (++ti[i] < tile) break;
+                            ti[i] = 0;
+                        }
+                        if (j == g.kh) break;
+                    }
                     int j = 0;
                     for (; j < g.kh; ++j) {
                         const int i = perm[j];
-                        if (++ti[i] < tile) break;
-                        ti[i] = 0;
+                        if (++to[i] < tr[i]) break;
+                        to[i] = 0;
                     }
                     if (j == g.kh) break;
                 }
-                int j = 0;
-                for (; j < g.kh; ++j) {
-                    const int i = perm[j];
-                    if (++to[i] < tr[i]) break;
-                    to[i] = 0;
-                }
-                if (j == g.kh) break;
-            }
-        } else {
-            // mixed-radix counter, perm[0] fastest; the packed digits come along
-            P.hdig.resize(g.nblocks);
-            std::vector<uint32_t> dig(g.kh, 0);
-            uint64_t h = 0, w = 0;
-            for (uint64_t n = 0; n < g.nblocks; ++n) {
-                const uint64_t q = fill[hl[h]]++;
-                P.hlist[q] = (uint32_t)h;
-                P.hdig[q] = w;
-                for (int j = 0; j < g.kh; ++j) {
-                    const int i = perm[j];
-                    if (++dig[i] < g.r[g.t + i]) {
-                        h += g.hcg[i];
-                        w += 1ull << (4 * i);
-                        break;
+            } else {
+                // mixed-radix counter, perm[0] fastest; the packed digits come along
+                P.hdig.resize(g.nblocks);
+                std::vector<uint32_t> dig(g.kh, 0);
+                uint64_t h = 0, w = 0;
+                for (uint64_t n = 0; n < g.nblocks; ++n) {
+                    const uint64_t q = fill[hl[h]]++;
+                    P.hlist[q] = (uint32_t)h;
+                    P.hdig[q] = w;
+                    for (int j = 0; j < g.kh; ++j) {
+                        const int i = perm[j];
+                        if (++dig[i] < g.r[g.t + i]) {
+                            h += g.hcg[i];
+                            w += 1ull << (4 * i);
+                            break;
+                        }
+                        h -= (uint64_t)(dig[i] - 1) * g.hcg[i];
+                        w &= ~(15ull << (4 * i));
+                        dig[i] = 0;
                     }
-                    h -= (uint64_t)(dig[i] - 1) * g.hcg[i];
-                    w &= ~(15ull << (4 * i));
-                    dig[i] = 0;
                 }
+            }
+            for (int s = 0; s <= hmax; ++s)
+                if (fill[s] != P.hoff[s + 1]) return "block order does not cover every block";
+            if (shuffled) P.hdig.clear();  // recomputed below for the shuffled list
+            if (shuffled)
+                for (int s = 0; s <= hmax; ++s) {  // experiment: shuffled (no reuse order)
+                    uint32_t *b = P.hlist.data() + P.hoff[s], *e = P.hlist.data() + P.hoff[s + 1];
+                    uint64_t x = 0x9E3779B97F4A7C15ull + (uint64_t)s;
+                    for (uint32_t *q = e; q - b > 1; --q) {
+                        x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+                        std::swap(q[-1], b[x % (uint64_t)(q - b)]);
+                    }
+                }
+        }
+        if (P.hdig.size() != g.nblocks) {  // experiment orders (tiled, shuffled)
+            P.hdig.resize(g.nblocks);
+            for (uint64_t q = 0; q < g.nblocks; ++q) {
+                uint64_t h = P.hlist[q], w = 0;
+                for (int i = 0; i < g.kh; ++i) w |= (uint64_t)kp_high_digit(g, h, i) << (4 * i);
+                P.hdig[q] = w;
             }
         }
-        for (int s = 0; s <= hmax; ++s)
-            if (fill[s] != P.hoff[s + 1]) return "block order does not cover every block";
-        const char *bo = getenv("KP_BLOCK_ORDER");
-        if (bo && atoi(bo) == 1) P.hdig.clear();  // recomputed below for the shuffled list
-        if (bo && atoi(bo) == 1)
-            for (int s = 0; s <= hmax; ++s) {  // experiment: shuffled (no reuse order)
-                uint32_t *b = P.hlist.data() + P.hoff[s], *e = P.hlist.data() + P.hoff[s + 1];
-                uint64_t x = 0x9E3779B97F4A7C15ull + (uint64_t)s;
-                for (uint32_t *q = e; q - b > 1; --q) {
-                    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-                    std::swap(q[-1], b[x % (uint64_t)(q - b)]);
-                }
-            }
-    }
-    if (P.hdig.size() != g.nblocks) {  // experiment orders (tiled, shuffled)
-        P.hdig.resize(g.nblocks);
+        P.kpos.resize(g.nblocks);
+        for (uint64_t q = 0; q < g.nblocks; ++q) P.kpos[P.hlist[q]] = (uint32_t)q;
+        P.hnp.resize(g.nblocks);
         for (uint64_t q = 0; q < g.nblocks; ++q) {
-            uint64_t h = P.hlist[q], w = 0;
-            for (int i = 0; i < g.kh; ++i) w |= (uint64_t)kp_high_digit(g, h, i) << (4 * i);
-            P.hdig[q] = w;
+            uint64_t n = 0;
+            for (int i = 0; i < g.kh; ++i) n |= (uint64_t)P.tabs[t + i].np[(P.hdig[q] >> (4 * i)) & 15u] << (3 * i);
+            P.hnp[q] = n;
         }
-    }
-    P.kpos.resize(g.nblocks);
-    for (uint64_t q = 0; q < g.nblocks; ++q) P.kpos[P.hlist[q]] = (uint32_t)q;
-    P.hnp.resize(g.nblocks);
-    for (uint64_t q = 0; q < g.nblocks; ++q) {
-        uint64_t n = 0;
-        for (int i = 0; i < g.kh; ++i) n |= (uint64_t)P.tabs[t + i].np[(P.hdig[q] >> (4 * i)) & 15u] << (3 * i);
-        P.hnp[q] = n;
-    }
+    }  // blocks_on_host
     // split pairs per position: sum over digits of np, times the other radices
     for (int i = 0; i < k; ++i) {
         double sum = 0;

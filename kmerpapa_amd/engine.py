@@ -64,7 +64,8 @@ EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_de
            "kp_plan_destroy", "kp_plan_get_info", "kp_plan_host", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
            "kp_reserve_lanes", "kp_last_pass_stats", "kp_last_launch_ms", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
            "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free",
-           "kp_format_long_rows", "kp_py_repr", "kp_device_groups", "kp_allkmers_cv"]
+           "kp_format_long_rows", "kp_py_repr", "kp_device_groups", "kp_allkmers_cv", "kp_block_order_check",
+           "kp_plan_block_check"]
 
 
 def load():
@@ -90,6 +91,8 @@ def load():
         L.kp_plan_destroy.restype = None
         L.kp_plan_get_info.argtypes = [vp, ctypes.POINTER(KPPlanInfo)]
         L.kp_plan_host.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(KPPlanInfo)]
+        L.kp_block_order_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32, u64p]
+        L.kp_plan_block_check.argtypes = [vp, u64p]
         L.kp_kmer_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                     ctypes.POINTER(vp)]
         L.kp_kmer_table_info.argtypes = [vp, u64p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64),
@@ -301,6 +304,15 @@ def plan_info(gen_pat, max_block=0):
     return {name: getattr(info, name) for name, _ in KPPlanInfo._fields_}
 
 
+def block_order_check(gen_pat, max_block=0):
+    """Blocks of ``gen_pat``'s lattice whose closed-form block-list slot (the rule the
+    device builds the list by, kp_blocks_kernel) differs from the host's block walk
+    (kp_block_order_check, host code): 0 when the two agree."""
+    n = ctypes.c_uint64()
+    _check(load().kp_block_order_check(gen_pat.encode(), ctypes.c_uint32(max_block), ctypes.byref(n)))
+    return n.value
+
+
 def _group_array(groups):
     """``groups`` (list of ``(fold, alpha, beta, penalties)``; ``beta`` may be a callable) as
     the C-ABI's kp_group array; returns it and the number of lanes."""
@@ -486,6 +498,13 @@ class Plan:
         s = KPPassStats()
         _check(load().kp_last_pass_stats(self._h, ctypes.byref(s)))
         return {name: getattr(s, name) for name, _ in KPPassStats._fields_}
+
+    def block_check(self):
+        """Entries of the device block list (built by kp_blocks_kernel) that differ from the
+        host's block walk (kp_plan_block_check): 0 when they agree."""
+        n = ctypes.c_uint64()
+        _check(load().kp_plan_block_check(self._h, ctypes.byref(n)))
+        return n.value
 
     def launch_ms(self):
         """Per-launch device times (ms) of the last pass (needs KP_LAUNCH_TIMES=1)."""

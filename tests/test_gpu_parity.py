@@ -89,6 +89,22 @@ def test_block_setup_without_pair_table(eng, monkeypatch, max_block):
         plan.close()
 
 
+@pytest.mark.parametrize("gen_pat,max_block,env", [
+    ("NNNNMNNNN", 0, None), ("RYSWKMBDHVN", 16, None), ("NNNNNNN", 16, None), ("NNNN", 0, None),
+    ("NNNNNNN", 16, ("KP_BLOCK_PERM", "3-0-5")), ("NNNNNNN", 16, ("KP_BLOCK_TILE", "2"))])
+def test_device_block_list_matches_host_walk(eng, monkeypatch, gen_pat, max_block, env):
+    """The plan's block list as the device builds it (kp_blocks_kernel: hlist, kpos, hdig,
+    hnp) equals the host's block walk entry for entry; KP_BLOCK_TILE (an experiment order
+    the host builds and uploads) goes through the same check."""
+    if env:
+        monkeypatch.setenv(*env)
+    plan = eng.Plan(eng.get_device(0), gen_pat, max_block)
+    try:
+        assert plan.block_check() == 0
+    finally:
+        plan.close()
+
+
 @pytest.mark.parametrize("case", ["k3", "k4", "k3zero", "k3big"])
 def test_small_lattice_fits(eng, case):
     from kmerpapa_amd.algorithms import bottum_up_array_w_numba as fitm
