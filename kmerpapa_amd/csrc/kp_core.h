@@ -73,7 +73,7 @@ __host__ __device__ inline double kp_lane_beta(const kp_group_dev &G, int j) {
 struct kp_geom {
     int k, t, kh;          // positions, low positions, high positions
     int nf;                // folds held in K (nf + 1 slots per k-mer-low cell, slot 0 = all data)
-    uint32_t B, Bpad;      // cells per block, padded row length (multiple of 16)
+    uint32_t B, Bpad;      // cells per block, padded row length (multiple of 32: 128-byte rows)
     uint32_t n_kl;         // k-mer-low cells per block
     uint32_t Ltot;         // lanes held in S / C
     uint64_t nblocks;      // number of blocks = npat / B

@@ -116,10 +116,15 @@ inline std::string build_plan(const char *gen_pat, uint32_t max_block, host_plan
     g.t = t;
     g.kh = k - t;
     g.B = (uint32_t)(t < k ? g.cgl[t] : acc);
-    {  // >= B + 1: slot B is the +inf cell of padded pair lists; a multiple of KP_BPAD_ALIGN floats
+    {
+        // row length of one block lane: >= B + 1 (slot B is the +inf cell of padded pair
+        // lists), a multiple of 32 floats so that every lane row starts on a 128-byte cache
+        // line (rows [h][lane] are back to back).  At 16 floats (64 B) half the rows of a
+        // 5-lane pass started mid-line: 9-mer pass 375 -> 366 ms at 32
+        // (profiles/r05/experiments/bpad_align.txt).  KP_BPAD_ALIGN=16/64/.. for experiments.
         const char *e = getenv("KP_BPAD_ALIGN");
-        uint32_t al = e ? (uint32_t)atoi(e) : 16u;
-        if (al < 16u || (al & (al - 1u))) al = 16u;
+        uint32_t al = e ? (uint32_t)atoi(e) : 32u;
+        if (al < 16u || (al & (al - 1u))) al = 32u;
         g.Bpad = (g.B + al) & ~(al - 1u);
     }
     g.nblocks = acc / g.B;

@@ -38,7 +38,7 @@ def test_require_lanes_message():
         big.require_lanes()
     assert e.value.code == -2
     msg = str(e.value)
-    assert "NNNNNNNNNR" in msg and "115,330,078,125 cells" in msg and "461.5 GB" in msg and "--super_pattern" in msg
+    assert "NNNNNNNNNR" in msg and "115,330,078,125 cells" in msg and "463.7 GB" in msg and "--super_pattern" in msg
     with pytest.raises(engine.KPError):
         engine.plan_passes([(0, 1.0, 1.0, [3.0])], 0, 5)
 
