@@ -135,12 +135,23 @@ def host_cores():
     return max(1, n)
 
 
-def cpu_baseline(prep):
+def pairs_per_cell(gen_pat):
+    """Split pairs per lattice cell (7.0 / 10.3 / 13.7 at the 5- / 7- /
+    9-mer): a CPU's cell rate falls with it, so every sample states its own."""
+    info = engine.plan_info(gen_pat)
+    return info["pairs_total"] / info["npat"]
+
+
+def cpu_baseline(prep, cores=None):
     """Time the CPU oracle on a bounded sample of the same counts: the sub-lattice with the
     two outermost ambiguous positions fixed to 'A' (3.4e7 cells for the 9-mer), one (alpha, c)
     over all folds per task.  Tasks run as the reference's README fans a grid out (one
-    independent single-threaded job per (alpha, c)), one per host core, concurrently; one
-    task alone on one core is reported beside it."""
+    independent single-threaded job per (alpha, c)), one per host core of this job's CPU
+    share, concurrently; one task alone on one core, and one task with its levels split
+    over every core by OpenMP (kpo_cv's threads), are reported beside it.  Every sample
+    states its split pairs per cell beside the workload's: the samples are smaller
+    lattices with fewer pairs per cell, so their cells/s overstate the CPU's rate on the
+    workload itself (about in the ratio of pairs per cell)."""
     from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle as O
     gp = prep["gen_pat"]
@@ -157,26 +168,39 @@ def cpu_baseline(prep):
     tasks = [(a, [beta[(a, f)] for f in range(nf)], c) for a in prep["alphas"] for c in prep["penalties"]]
     O.lib()
 
-    def one(task):
+    def one(task, threads=1):
         a, betas, c = task
-        O.cv_pass(sub, ctxs, Mf, Uf, a, betas, c, bits)  # ctypes drops the GIL: tasks run in parallel
+        O.cv_pass(sub, ctxs, Mf, Uf, a, betas, c, bits, threads=threads)  # ctypes drops the GIL
     t0 = time.time()
     one(tasks[0])
     t1 = time.time() - t0
-    cores = host_cores()
+    cores = cores or host_cores()
+    online = os.cpu_count()
     # memory: ~4.1 GB per concurrent 9-mer sample task
     par = max(1, min(cores, len(tasks)))
     t0 = time.time()
     with ThreadPoolExecutor(par) as ex:
         list(ex.map(one, [tasks[i % len(tasks)] for i in range(par)]))
     tn = time.time() - t0
+    t0 = time.time()
+    one(tasks[0], threads=cores)
+    tomp = time.time() - t0
     units = O.npat(sub) * nf
+    share = (f"{cores} = this job's CPU share of the {online}-CPU host (OMP_NUM_THREADS, set by the GPU pool "
+             f"for one GPU; the host's other CPUs serve its other GPUs)") if online and online > cores else \
+        f"{cores} = every online CPU"
     return {"value": units * par / tn, "unit": "cells*folds*(alpha,c)/s", "cores": par, "kind": "port",
-            "host_cpus_online": os.cpu_count(),
+            "host_cpus_online": online, "cpu_share": share,
+            "all_cpus_extrapolated": (units * par / tn) / par * online if online else None,
             "single_core_value": units / t1,
+            "sample_pairs_per_cell": pairs_per_cell(sub), "workload_pairs_per_cell": pairs_per_cell(gp),
             "sample": f"oracle/kp_oracle.c kpo_cv (1 thread per task) on sub-lattice {sub} of the same counts "
-                      f"({O.npat(sub)} cells x {nf} folds per (alpha,c) task): {par} concurrent tasks on "
+                      f"({O.npat(sub)} cells x {nf} folds per (alpha,c) task, {pairs_per_cell(sub):.2f} split pairs "
+                      f"per cell against the workload's {pairs_per_cell(gp):.2f}): {par} concurrent tasks on "
                       f"{par} host cores in {tn:.1f} s; 1 task alone on 1 core in {t1:.1f} s",
+            "openmp": {"value": units / tomp, "threads": cores,
+                       "sample": f"kpo_cv, one (alpha,c) task on {sub} with each level's cells split over "
+                                 f"{cores} OpenMP threads: {tomp:.1f} s"},
             "python": python_baseline(prep, tasks, par)}
 
 
@@ -214,11 +238,15 @@ def python_baseline(prep, tasks, par):
             raise RuntimeError("pure-Python baseline task failed")
     secs = [float(o.split()[-1]) for o in outs]
     units = O.npat(sub) * nf
+    online = os.cpu_count()
     return {"value": units * par / tn, "unit": "cells*folds*(alpha,c)/s", "cores": par,
             "kind": "reference-equivalent pure Python (oracle/pyref.py)",
             "single_core_value": units / (sum(secs) / len(secs)),
+            "all_cpus_extrapolated": (units * par / tn) / par * online if online else None,
+            "sample_pairs_per_cell": pairs_per_cell(sub), "workload_pairs_per_cell": pairs_per_cell(gp),
             "sample": f"oracle/pyref.py cv_pass on sub-lattice {sub} of the same counts ({O.npat(sub)} cells x "
-                      f"{nf} folds per (alpha,c) task): {par} processes on {par} host cores in {tn:.1f} s "
+                      f"{nf} folds per (alpha,c) task, {pairs_per_cell(sub):.2f} split pairs per cell against the "
+                      f"workload's {pairs_per_cell(gp):.2f}): {par} processes on {par} host cores in {tn:.1f} s "
                       f"(per task {min(secs):.1f}-{max(secs):.1f} s)"}
 
 
@@ -461,6 +489,8 @@ def main():
                     help="9mer = BASELINE configs[3] (the headline); 11mer = configs[4] (super-pattern restricted)")
     ap.add_argument("--pattern", default=None, help="override the config's general pattern")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="host cores for the CPU baseline (default: this job's CPU share, host_cores())")
     ap.add_argument("--max-block", type=int, default=0)
     ap.add_argument("--no-full-cv", action="store_true", help="skip the full grid CV wall-clock leg")
     ap.add_argument("--model-worlds", default="2,4,8",
@@ -603,7 +633,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (scores, split sums) + f64 (single-pattern term); u32 counts",
+            "dtype": f"f32 (scores, split sums) + f64 (single-pattern term); "
+                     f"u{8 * np.dtype(prep['itype']).itemsize} counts",
             "data": "synthetic",
             "config": {"workload": f"synthetic {len(gen_pat)}-mer counts, general pattern {gen_pat} "
                                    f"({plan.info['npat']} cells), {len(prep['alphas'])}x{len(prep['penalties'])} "
@@ -632,7 +663,7 @@ def main():
                 line["cv_full_grid_speedup_model_8gpu"] = cv["models"]["8"]["speedup"]
         if not a.no_cpu_baseline and world == 1:
             note("cpu baseline")
-            line["cpu_baseline"] = cpu_baseline(prep)
+            line["cpu_baseline"] = cpu_baseline(prep, a.cpu_cores or None)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)

@@ -103,6 +103,10 @@ int kp_plan_get_info(const kp_plan *plan, kp_plan_info *out);
 /* Host-only (no GPU): build the plan's tables on the host and report their info -- the
  * lattice size and device bytes per lane a job would need, before any device is touched. */
 int kp_plan_host(const char *gen_pat, uint32_t max_block, kp_plan_info *out);
+/* The same at count width itype_bytes (4 or 8, CV :94-97's itype): lanes_per_workgroup is
+ * then the width kp_pass cuts device groups by on an MI355X (160 KiB of LDS per CU), the
+ * group size a multi-GPU job deals whole to its ranks. */
+int kp_plan_host_counts(const char *gen_pat, uint32_t max_block, int itype_bytes, kp_plan_info *out);
 /* Checks of the block list (test hooks; no reference counterpart).  The device builds the
  * plan's block list (blocks by high level) from a closed-form rank rule.
  * kp_block_order_check, host-only: *mismatches = blocks whose closed-form slot differs from

@@ -462,6 +462,7 @@ struct kp_ctx {
 struct kp_plan {
     kp_ctx *ctx = nullptr;
     kp::host_plan hp;
+    uint32_t max_block = 4096;  // the block budget build_plan ran with (kp_plan_block_check rebuilds with it)
     // device tables
     kp_postab *d_tabs = nullptr;
     uint32_t *d_lowinfo = nullptr;
@@ -643,6 +644,9 @@ static int device_blocks(kp_plan *p) {
     }
     dfree(d_brank);
     dfree(d_hoff);
+    if (he == hipErrorOutOfMemory)  // the block-list tables do not fit: the lattice is too big here
+        return fail(KP_E_NOMEM, "block list of " + p->hp.gp + " (" + std::to_string(g.nblocks) +
+                                    " blocks): out of device memory");
     if (he != hipSuccess) return fail(KP_E_HIP, std::string("block list: ") + hipGetErrorString(he));
     return KP_OK;
 }
@@ -654,7 +658,8 @@ int kp_plan_create(kp_ctx *ctx, const char *gen_pat, uint32_t max_block, kp_plan
     KP_HIP(hipSetDevice(ctx->device));
     kp_plan *p = new kp_plan();
     p->ctx = ctx;
-    std::string err = kp::build_plan(gen_pat, max_block ? max_block : 4096u, p->hp, false);
+    p->max_block = max_block ? max_block : 4096u;
+    std::string err = kp::build_plan(gen_pat, p->max_block, p->hp, false);
     if (!err.empty()) {
         delete p;
         return fail(KP_E_ARG, err);
@@ -771,6 +776,15 @@ int kp_plan_host(const char *gen_pat, uint32_t max_block, kp_plan_info *o) {
     return KP_OK;
 }
 
+int kp_plan_host_counts(const char *gen_pat, uint32_t max_block, int itype_bytes, kp_plan_info *o) {
+    if (!gen_pat || !o || (itype_bytes != 4 && itype_bytes != 8)) return fail(KP_E_ARG, "bad arguments");
+    kp::host_plan hp;
+    std::string err = kp::build_plan(gen_pat, max_block ? max_block : 4096u, hp, false);
+    if (!err.empty()) return fail(KP_E_ARG, err);
+    info_of(hp, o, (size_t)itype_bytes);
+    return KP_OK;
+}
+
 // Host-only (no GPU): the closed-form block order (kp_block_slot) against build_plan's
 // block walk, every block of the lattice; *mismatches = blocks whose slot, digits or
 // split-pair counts differ.
@@ -800,18 +814,11 @@ int kp_block_order_check(const char *gen_pat, uint32_t max_block, uint64_t *mism
 int kp_plan_block_check(kp_plan *p, uint64_t *mismatches) {
     if (!p || !mismatches) return fail(KP_E_ARG, "null argument");
     KP_HIP(hipSetDevice(p->ctx->device));
-    kp::host_plan hp;
-    std::string err = kp::build_plan(p->hp.gp.c_str(), 0, hp, true);
+    kp::host_plan hp;  // the host walk with the plan's own block budget
+    std::string err = kp::build_plan(p->hp.gp.c_str(), p->max_block, hp, true);
     if (!err.empty()) return fail(KP_E_ARG, err);
-    if (hp.g.nblocks != p->hp.g.nblocks || hp.g.B != p->hp.g.B) {  // built with another block budget
-        kp::host_plan h2;
-        for (uint32_t mb = 1; mb <= 65536u; mb *= 2) {
-            if (!kp::build_plan(p->hp.gp.c_str(), mb, h2, true).empty()) continue;
-            if (h2.g.B == p->hp.g.B) break;
-        }
-        if (h2.g.B != p->hp.g.B) return fail(KP_E_ARG, "cannot rebuild the plan's block size");
-        hp = std::move(h2);
-    }
+    if (hp.g.nblocks != p->hp.g.nblocks || hp.g.B != p->hp.g.B)
+        return fail(KP_E_ARG, "the host walk does not rebuild the plan's block size");
     const uint64_t n = hp.g.nblocks;
     std::vector<uint32_t> hl(n), kp(n);
     std::vector<uint64_t> hd(n), hn(n);

@@ -61,7 +61,7 @@ class KPPassStats(ctypes.Structure):
 
 
 EXPORTS = ["kp_last_error", "kp_device_count", "kp_create", "kp_destroy", "kp_device_mem", "kp_plan_create",
-           "kp_plan_destroy", "kp_plan_get_info", "kp_plan_host", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
+           "kp_plan_destroy", "kp_plan_get_info", "kp_plan_host", "kp_plan_host_counts", "kp_set_counts", "kp_counts_begin", "kp_counts_fold", "kp_pass",
            "kp_reserve_lanes", "kp_last_pass_stats", "kp_last_launch_ms", "kp_fit_leaves", "kp_dump_lane", "kp_gather_cells", "kp_fold_split",
            "kp_fold_sample", "kp_math_log", "kp_math_libm", "kp_kmer_parse", "kp_kmer_table_info", "kp_kmer_table_copy", "kp_kmer_table_free",
            "kp_format_long_rows", "kp_py_repr", "kp_device_groups", "kp_allkmers_cv", "kp_block_order_check",
@@ -91,6 +91,7 @@ def load():
         L.kp_plan_destroy.restype = None
         L.kp_plan_get_info.argtypes = [vp, ctypes.POINTER(KPPlanInfo)]
         L.kp_plan_host.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(KPPlanInfo)]
+        L.kp_plan_host_counts.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(KPPlanInfo)]
         L.kp_block_order_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32, u64p]
         L.kp_plan_block_check.argtypes = [vp, u64p]
         L.kp_kmer_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
@@ -302,6 +303,23 @@ def plan_info(gen_pat, max_block=0):
     info = KPPlanInfo()
     _check(load().kp_plan_host(gen_pat.encode(), ctypes.c_uint32(max_block), ctypes.byref(info)))
     return {name: getattr(info, name) for name, _ in KPPlanInfo._fields_}
+
+
+def shard_width(gen_pat, itype=np.uint32, max_block=0):
+    """Lanes one sweep workgroup holds for ``gen_pat``'s lattice at count width ``itype``
+    (kp_plan_host_counts, host only): the group size shard.assign_lanes deals whole.  A pure
+    function of the lattice and the count width, so every rank of a job computes the same."""
+    info = KPPlanInfo()
+    _check(load().kp_plan_host_counts(gen_pat.encode(), ctypes.c_uint32(max_block), int(np.dtype(itype).itemsize),
+                                      ctypes.byref(info)))
+    return int(info.lanes_per_workgroup)
+
+
+def counts_itype(M):
+    """Count width of a run's counts: an array, a FoldFeed, or None (uint32)."""
+    if isinstance(M, FoldFeed):
+        return M.M_all.dtype
+    return np.asarray(M).dtype if M is not None else np.dtype(np.uint32)
 
 
 def block_order_check(gen_pat, max_block=0):
@@ -555,7 +573,8 @@ class Plan:
             raise KPError(-2, f"the lattice of {self.gen_pat} ({self.info['npat']:,} cells) needs "
                               f"{per / 1e9:.4g} GB of device memory per lane (float32 score per cell), "
                               f"{n} lane(s) at least; GPU {self.device.device} has {(fr + self.lanes_held * per) / 1e9:.4g} "
-                              f"of {tot / 1e9:.4g} GB free after the plan's tables. Restrict the general pattern "
+                              f"of {tot / 1e9:.4g} GB free after the plan's tables, of which {reserve / 2**30:.3g} GiB "
+                              f"stay free for the library's working buffers. Restrict the general pattern "
                               f"with --super_pattern.")
         return fit
 
@@ -847,9 +866,9 @@ def _shutdown():
 atexit.register(_shutdown)
 
 
-def _device_shares(groups, devices):
+def _device_shares(groups, devices, width):
     from .shard import rank_groups
-    return [rank_groups(groups, slot, len(devices)) for slot in range(len(devices))]
+    return [rank_groups(groups, slot, len(devices), width) for slot in range(len(devices))]
 
 
 def _replicas(devices):
@@ -864,12 +883,14 @@ def _replicas(devices):
     return out
 
 
-def prepare_groups(gen_pat, groups, devices=None, max_block=0):
+def prepare_groups(gen_pat, groups, devices=None, max_block=0, itype=np.uint32):
     """Everything ``run_groups`` needs before the counts exist: each GPU's plan (lattice
     tables uploaded) and one allocation for its largest pass.  Only the lane counts of
     ``groups`` matter (folds, alphas and betas may be placeholders), so a caller can run
-    this while the host draws the fold split (CV_tools.fold_tables drops the GIL)."""
+    this while the host draws the fold split (CV_tools.fold_tables drops the GIL).  ``itype``
+    = the counts' width to come (the shares depend on it, shard_width)."""
     devices = list(devices if devices is not None else visible_devices()[:1])
+    width = shard_width(gen_pat, itype, max_block) if len(devices) > 1 else 0
 
     errors = []
 
@@ -883,7 +904,7 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0):
         except Exception as e:  # re-raised in the caller's thread
             errors.append(e)
     threads = [threading.Thread(target=prep, args=(dev, rep, chunk))
-               for dev, rep, chunk in zip(devices, _replicas(devices), _device_shares(groups, devices))]
+               for dev, rep, chunk in zip(devices, _replicas(devices), _device_shares(groups, devices, width))]
     for th in threads:
         th.start()
     for th in threads:
@@ -913,7 +934,9 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     if not devices:
         raise KPError(-3, "no GPU visible")
     nd = len(devices)
-    shares = _device_shares(groups, devices)  # (results go back to lane order by shard.unshard)
+    # (whole groups of one workgroup's width per device; results go back by shard.unshard)
+    width = shard_width(gen_pat, counts_itype(M), max_block) if nd > 1 else 0
+    shares = _device_shares(groups, devices, width)
     results = [None] * nd
     errors = []
 
@@ -993,7 +1016,7 @@ def run_groups(gen_pat, M, U, groups, devices=None, max_block=0):
     if errors:
         raise errors[0]
     from .shard import unshard
-    return tuple(unshard(groups, nd, [r[i] for r in results]) for i in range(3))
+    return tuple(unshard(groups, nd, [r[i] for r in results], width) for i in range(3))
 
 
 run_groups.prepare = prepare_groups

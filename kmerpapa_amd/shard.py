@@ -28,7 +28,9 @@ def chunk_bounds(lane_counts, parts):
     return bounds
 
 
-# lanes one sweep workgroup holds with 32-bit counts (kp_plan_info.lanes_per_workgroup)
+# lanes one sweep workgroup holds at 9-mer size with 32-bit counts
+# (kp_plan_info.lanes_per_workgroup); callers pass the lattice's own width at its count
+# width (engine.shard_width: 4 with 64-bit counts, fewer for lattices with larger blocks)
 WG_LANES = 5
 
 
@@ -116,30 +118,39 @@ def fold_order(nf):
     return list(range(1, nf)) + [0] if nf > 1 else [0]
 
 
-def sharded_run_groups(run_groups, rank, world, all_gather, devices=None):
+def sharded_run_groups(run_groups, rank, world, all_gather, devices=None, width=None):
     """Wrap a ``run_groups(gen_pat, M, U, groups, devices, max_block)`` callable so that
     each rank runs only its chunk and every rank returns the full lane arrays.
 
     ``all_gather(obj) -> list`` collects one picklable object per rank, in rank order
-    (e.g. ``torch.distributed.all_gather_object``).
+    (e.g. ``torch.distributed.all_gather_object``).  ``width`` = the group size dealt whole
+    (assign_lanes); None = the lattice's sweep-workgroup width at the counts' width
+    (engine.shard_width, the same on every rank).
     """
     fixed = devices
 
+    def _width(gen_pat, M, max_block):
+        if width is not None:
+            return width
+        from . import engine
+        return engine.shard_width(gen_pat, engine.counts_itype(M), max_block)
+
     def prepare(gen_pat, groups, devices=None, max_block=0):
         inner = getattr(run_groups, "prepare", None)
-        mine = rank_groups(groups, rank, world)
+        mine = rank_groups(groups, rank, world, _width(gen_pat, None, max_block))
         if inner is not None and mine:
             inner(gen_pat, mine, devices=fixed if fixed is not None else devices, max_block=max_block)
 
     def run(gen_pat, M, U, groups, devices=None, max_block=0):
-        mine = rank_groups(groups, rank, world)
+        w = _width(gen_pat, M, max_block)
+        mine = rank_groups(groups, rank, world, w)
         if mine:
             rt, re, nl = run_groups(gen_pat, M, U, mine, devices=fixed if fixed is not None else devices,
                                     max_block=max_block)
         else:
             rt, re, nl = np.zeros(0, np.float32), np.zeros(0, np.float32), np.zeros(0, np.uint64)
         parts = all_gather((np.asarray(rt), np.asarray(re), np.asarray(nl)))
-        return tuple(unshard(groups, world, [p[i] for p in parts]) for i in range(3))
+        return tuple(unshard(groups, world, [p[i] for p in parts], w) for i in range(3))
     run.prepare = prepare
     run.fold_feed = getattr(run_groups, "fold_feed", False)
     return run

@@ -213,6 +213,136 @@ int kpo_cv(const char *gp, int nf, uint64_t *M, uint64_t *U, int itype_bits,
 }
 
 /*
+ * One CV lane over a whole lattice, memory-lean: the train score of every cell for ONE fold
+ * (train counts = all data - that fold, CV :22-24, :56-59) and one (alpha, beta_f, penalty),
+ * the same per-cell recurrence as kpo_cv (CV :15-20 at k-mers, :26-71 above) -- the train
+ * scores of a lane depend on nothing else (the test array only feeds test_score_mem).
+ * Memory: the score array (caller's, float32 [npat]) + train counts of every cell
+ * (uint32 when ``itype_bits`` is 32, else uint64), 12 B/cell at 32 bits: a 7.7e9-cell
+ * 9-mer lane in 92 GB, where kpo_cv's [npat][nf] layout would need 38 B/cell/fold.
+ * Counts are aggregated over the first split pair like the reference (CV :52-55); with the
+ * reference's itype rule (CV :94-97: uint32 only if all counts sum below 2^32) no cell's
+ * train count can wrap, so summing train counts equals summing folds and subtracting.
+ *   kcell[n_kmers]: cell index of each k-mer; m, u: its train counts.
+ * Cells are walked level by level, each level's cells split over OpenMP threads through a
+ * low/high decomposition of the index (no [npat] level-order array): low = the first
+ * positions whose radix product is <= 4096, a cell's level = low level + high level.
+ */
+#define KPO_LANE_BODY(CT)                                                                              \
+    do {                                                                                               \
+        CT *M = (CT *)calloc(L.npat, sizeof(CT)), *U = (CT *)calloc(L.npat, sizeof(CT));              \
+        if (!M || !U) { free(M); free(U); rc = -2; break; }                                           \
+        for (uint64_t j = 0; j < n_kmers; ++j) { M[kcell[j]] = (CT)m[j]; U[kcell[j]] = (CT)u[j]; }      \
+        for (int lev = 0; lev <= L.maxlev; ++lev) {                                                    \
+            _Pragma("omp parallel for num_threads(nt) schedule(dynamic, 64)")                          \
+            for (uint64_t h = 0; h < nhi; ++h) {                                                       \
+                const int ll = lev - (int)hlev[h];                                                     \
+                if (ll < 0 || ll > lomax) continue;                                                    \
+                int dg[KPO_MAXK];                                                                      \
+                uint64_t hq = h;                                                                       \
+                for (int i = t; i < L.k; ++i) { dg[i] = (int)(hq % L.radix[i]); hq /= L.radix[i]; }    \
+                for (uint64_t q = looff[ll]; q < looff[ll + 1]; ++q) {                                 \
+                    const uint64_t n = h * B + lolist[q];                                              \
+                    if (lev == 0) { /* a k-mer: score_test_folds (CV :15-20) */                        \
+                        const uint64_t trm = M[n], tru = U[n];                                         \
+                        double p = ((double)trm + alpha) / (((double)(trm + tru) + alpha) + beta);     \
+                        score[n] = (float)(-2.0 * (xlogy_((double)trm, p) + xlog1py_((double)tru, -p)) \
+                                           + penalty);                                                 \
+                        continue;                                                                      \
+                    }                                                                                  \
+                    float rs = inf32;                                                                  \
+                    int first = 1;                                                                     \
+                    for (int i = 0; i < t; ++i) dg[i] = lodig[lolist[q] * (uint64_t)t + i];           \
+                    for (int i = 0; i < L.k; ++i) {                                                    \
+                        const int d = dg[i];                                                           \
+                        for (int j = 0; j < L.np[i][d]; ++j) {                                         \
+                            uint64_t base = n - (uint64_t)d * L.cg[i];                                 \
+                            uint64_t c1 = base + (uint64_t)L.pa[i][d][j] * L.cg[i];                    \
+                            uint64_t c2 = base + (uint64_t)L.pb[i][d][j] * L.cg[i];                    \
+                            float ns = score[c1] + score[c2];                                          \
+                            if (ns < rs) rs = ns;                                                      \
+                            if (first) { M[n] = M[c1] + M[c2]; U[n] = U[c1] + U[c2]; first = 0; }      \
+                        }                                                                              \
+                    }                                                                                  \
+                    const uint64_t trm = M[n], tru = U[n];                                             \
+                    double p = ((double)trm + alpha) / (((double)(trm + tru) + alpha) + beta);         \
+                    double s = penalty;                                                                \
+                    if (trm > 0) s += (-2.0 * (double)trm) * log(p);                                   \
+                    if (tru > 0) s += (-2.0 * (double)tru) * log(1.0 - p);                             \
+                    score[n] = (s < (double)rs) ? (float)s : rs;                                       \
+                }                                                                                      \
+            }                                                                                          \
+        }                                                                                              \
+        free(M);                                                                                       \
+        free(U);                                                                                       \
+    } while (0)
+
+int kpo_cv_lane(const char *gp, uint64_t n_kmers, const uint64_t *kcell, const uint64_t *m, const uint64_t *u,
+                int itype_bits, double alpha, double beta, double penalty, float *score, int nthreads) {
+    kpo_lat L;
+    if (lat_build(gp, &L)) return -1;
+    for (uint64_t j = 0; j < n_kmers; ++j)
+        if (kcell[j] >= L.npat) return -1;
+    const float inf32 = (float)1e100;
+    const int nt = nthreads > 0 ? nthreads : 1;
+    /* low positions 0..t-1 (radix product B <= 4096), high = the rest */
+    int t = 0;
+    uint64_t B = 1;
+    while (t < L.k && B * (uint64_t)L.radix[t] <= 4096) B *= (uint64_t)L.radix[t++];
+    const uint64_t nhi = L.npat / B;
+    int lomax = 0;
+    for (int i = 0; i < t; ++i) lomax += L.lev[i][L.radix[i] - 1];
+    uint64_t looff[KPO_MAXK * 3 + 2] = {0};
+    uint32_t *lolist = (uint32_t *)malloc(sizeof(uint32_t) * B);
+    uint8_t *hlev = (uint8_t *)malloc(nhi ? nhi : 1);
+    uint8_t *lodig = (uint8_t *)malloc(B * (uint64_t)(t ? t : 1));
+    if (!lolist || !hlev || !lodig) { free(lolist); free(hlev); free(lodig); return -2; }
+    for (uint64_t x = 0; x < B; ++x) {
+        uint64_t q = x;
+        for (int i = 0; i < t; ++i) { lodig[x * t + i] = (uint8_t)(q % L.radix[i]); q /= L.radix[i]; }
+    }
+    for (uint64_t x = 0; x < B; ++x) {  /* low cells bucketed by low level, ascending */
+        uint64_t q = x;
+        int s = 0;
+        for (int i = 0; i < t; ++i) { s += L.lev[i][q % L.radix[i]]; q /= L.radix[i]; }
+        looff[s + 1]++;
+    }
+    for (int s = 0; s <= lomax; ++s) looff[s + 1] += looff[s];
+    {
+        uint64_t fill[KPO_MAXK * 3 + 2] = {0};
+        for (uint64_t x = 0; x < B; ++x) {
+            uint64_t q = x;
+            int s = 0;
+            for (int i = 0; i < t; ++i) { s += L.lev[i][q % L.radix[i]]; q /= L.radix[i]; }
+            lolist[looff[s] + fill[s]++] = (uint32_t)x;
+        }
+    }
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (uint64_t h = 0; h < nhi; ++h) {
+        uint64_t q = h;
+        int s = 0;
+        for (int i = t; i < L.k; ++i) { s += L.lev[i][q % L.radix[i]]; q /= L.radix[i]; }
+        hlev[h] = (uint8_t)s;
+    }
+#pragma omp parallel for num_threads(nt) schedule(static)
+    for (uint64_t n = 0; n < L.npat; ++n) score[n] = inf32;
+    int rc = 0;
+    if (itype_bits <= 32) KPO_LANE_BODY(uint32_t);
+    else KPO_LANE_BODY(uint64_t);
+    free(lolist);
+    free(hlev);
+    free(lodig);
+    return rc;
+}
+
+/* the host C library's log / log1p over an array (fn 0 / 1): what numba's np.log / np.log1p
+ * lower to and what scipy's xlogy / xlog1py multiply (oracle/treecheck.py's vectorised
+ * single terms) */
+void kpo_libm_array(const double *x, double *y, uint64_t n, int fn) {
+    for (uint64_t i = 0; i < n; ++i) y[i] = fn ? log1p(x[i]) : log(x[i]);
+}
+
+/*
  * Fit DP (one fold, full data) with back-pointers.
  *   M, U      : [npat]; k-mer rows are inputs, the rest outputs.
  *   score     : [npat] float32 output, backtrack : [npat] output (c1 of the winning split,

@@ -50,6 +50,11 @@ def lib():
         L.kpo_fit.argtypes = [ctypes.c_char_p, u64p, u64p, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                               ctypes.c_double, f32p, u64p, ctypes.c_int]
         L.kpo_fit.restype = ctypes.c_int
+        L.kpo_cv_lane.argtypes = [ctypes.c_char_p, ctypes.c_uint64, u64p, u64p, u64p, ctypes.c_int,
+                                  ctypes.c_double, ctypes.c_double, ctypes.c_double, f32p, ctypes.c_int]
+        L.kpo_cv_lane.restype = ctypes.c_int
+        L.kpo_libm_array.argtypes = [f64p, f64p, ctypes.c_uint64, ctypes.c_int]
+        L.kpo_libm_array.restype = None
         _lib = L
     return _lib
 
@@ -109,6 +114,33 @@ def cv_pass(gen_pat, contexts, Mf, Uf, alpha, betas, penalty, itype_bits=32, thr
     root = cell_index(gen_pat, gen_pat)
     return {"score": score, "test": test, "M": M, "U": U,
             "root_train": score[root].copy(), "root_test": test[root].copy()}
+
+
+def cv_lane(gen_pat, kcell, m, u, alpha, beta, penalty, itype_bits=32, threads=1, out=None):
+    """Train scores (float32 ``[npat]``, reference cell order) of ONE CV lane over the whole
+    lattice of ``gen_pat`` (kpo_cv_lane: the kpo_cv recurrence for one fold, train counts
+    only, 12 B/cell).  ``kcell`` = cell index of each k-mer, ``m``/``u`` = its train counts
+    (all data - the lane's fold).  ``out`` may be a preallocated float32 array."""
+    kcell = np.ascontiguousarray(kcell, dtype=np.uint64)
+    m = np.ascontiguousarray(m, dtype=np.uint64)
+    u = np.ascontiguousarray(u, dtype=np.uint64)
+    n = npat(gen_pat)
+    score = np.empty(n, np.float32) if out is None else out
+    assert score.dtype == np.float32 and score.size == n and score.flags.c_contiguous
+    rc = lib().kpo_cv_lane(gen_pat.encode(), kcell.size, _ptr(kcell, ctypes.c_uint64), _ptr(m, ctypes.c_uint64),
+                           _ptr(u, ctypes.c_uint64), int(itype_bits), float(alpha), float(beta), float(penalty),
+                           _ptr(score, ctypes.c_float), int(threads))
+    if rc:
+        raise RuntimeError(f"kpo_cv_lane failed ({rc})")
+    return score
+
+
+def libm(x, fn="log"):
+    """The host C library's ``log`` / ``log1p`` over a float64 array."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().kpo_libm_array(_ptr(x, ctypes.c_double), _ptr(y, ctypes.c_double), x.size, 1 if fn == "log1p" else 0)
+    return y
 
 
 def _right(super_pat, left):

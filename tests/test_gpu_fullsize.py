@@ -259,7 +259,7 @@ def _leaf_kmers(gen_pat, leaves):
     return leaf, kidx
 
 
-def _tree_check_pass(plan, lat, groups, Mk, Uk, rt, re, nl):
+def _tree_check_pass(plan, lat, groups, Mk, Uk, rt, re, nl, offtree=(), stats=None):
     """Every lane of the pass just run (``groups``, lanes group-major): the host walks the
     lane's optimal tree top-down from the GPU's stored train scores (oracle/treecheck.py:
     split candidates in the reference's scan order with the first minimum winning, the
@@ -268,7 +268,10 @@ def _tree_check_pass(plan, lat, groups, Mk, Uk, rt, re, nl):
     one bit for bit; the root's train and test values returned by the pass must equal the
     re-derived root (test = the float32 sums test[c1] + test[c2] along the tree, CV :47,
     :158-163) and kp_fit_leaves the re-derived leaves in backtrack order.  The leaves
-    must also cover every k-mer exactly once.  Returns the number of tree nodes checked."""
+    must also cover every k-mer exactly once.  Lanes in ``offtree`` also re-derive every
+    split candidate of every tree node one level down (treecheck ``offtree``: the cells the
+    tree's first minima were taken against).  Returns the number of tree nodes checked;
+    ``stats`` (a dict) accumulates nodes, candidates and lanes."""
     from oracle import treecheck as T
     Mall, Uall = Mk.sum(axis=1), Uk.sum(axis=1)
     lane, nodes = 0, 0
@@ -276,7 +279,12 @@ def _tree_check_pass(plan, lat, groups, Mk, Uk, rt, re, nl):
         mte, ute = Mk[:, fold], Uk[:, fold]
         for c in pens:
             r = T.rederive(lat, lambda cells, j=lane: plan.gather_cells(j, cells), Mall - mte, Uall - ute,
-                           mte, ute, a, float(b), c)
+                           mte, ute, a, float(b), c, offtree=lane in offtree)
+            if stats is not None:
+                stats["nodes"] = stats.get("nodes", 0) + r["nodes"]
+                stats["candidates"] = stats.get("candidates", 0) + r["candidates"]
+                stats["lanes"] = stats.get("lanes", 0) + 1
+                stats["offtree_lanes"] = stats.get("offtree_lanes", 0) + (lane in offtree)
             where = (fold, a, c)
             assert r["root_train"].view(np.uint32) == np.float32(rt[lane]).view(np.uint32), where
             assert r["root_test"].view(np.uint32) == np.float32(re[lane]).view(np.uint32), where
@@ -287,6 +295,10 @@ def _tree_check_pass(plan, lat, groups, Mk, Uk, rt, re, nl):
             nodes += r["nodes"]
             lane += 1
     return nodes
+
+
+_GRID9 = {}  # (fold, alpha, c) -> (root train, root test, leaves) of the one-GPU 5x5x5 run
+ALPHAS9, PENS9 = [0.5, 1.0, 2.0, 5.0, 10.0], [3.0, 4.0, 5.0, 6.0, 7.0]
 
 
 @pytest.mark.timeout(1200)
@@ -314,6 +326,8 @@ def test_9mer_full_cv_all_125_lanes_tree_rederived(cv_split):
             rt, re, nl = plan.run(grp)
             nodes += _tree_check_pass(plan, lat, grp, Mk, Uk, rt, re, nl)
             lanes += len(pens)
+            for j, c in enumerate(pens):  # the one-GPU job's roots, for the 8-rank shares below
+                _GRID9[(f, a, c)] = (rt[j], re[j], nl[j])
     assert lanes == 125
     print(f"9-mer grid: {lanes} lanes, {nodes} tree nodes re-derived")
 
@@ -499,4 +513,192 @@ def test_11mer_full_mixed_fold_piece_fold_feed_vs_oracle():
         tuple((g[0], g[1], g[2], list(g[3])) for g in piece)) == 1  # a pass of the grid's own plan
     assert engine.device_groups(piece, 5) == [(0, 5, 2)]  # one workgroup, last 2 lanes on the second alpha
     _fed_pass_vs_oracle(gp, ctx, nf, piece, SUBS11)
+    engine.release_all()
+
+
+# ---------------------------------------------------------------------------------------
+# The 8-GPU job's own passes at full size.  An 8-rank CV job (torchrun, one process per GPU;
+# the in-job replacement for the reference's README fan-out, README.md:39-51) gives every
+# rank a lane-granular share of the grid (shard.rank_groups) and runs it as
+# engine.plan_passes cuts it with pass_cap = one workgroup + 1 lane: at 9-mers every
+# 16-lane share is [5], [5], [5 + 1], the last a packed pass of two folds whose odd lane
+# reads another fold's count-table row in the same launches.  Here one GPU runs exactly
+# those passes, rank after rank; every lane of ranks 0 and 7 is tree-checked with the
+# off-tree candidates, one packed odd lane is compared cell by cell over the WHOLE lattice
+# with the oracle, and shard.unshard of the eight ranks' roots must equal the one-GPU
+# job's roots bit for bit.
+# ---------------------------------------------------------------------------------------
+
+def _kmer_cells(lat):
+    """Cell index of every k-mer (k-mer index order): digit = position of the k-mer's
+    nucleotide in perm_code of the general code (oracle tables)."""
+    from oracle.oracle import _PERM
+    cells = np.zeros(lat.n_kmers, np.uint64)
+    for i, g in enumerate(lat.gp):
+        lut = np.array([_PERM[g].index(n) for n in IUPAC[g]], np.uint64)
+        cells += lut[lat.kdig[i]] * np.uint64(lat.cw[i])
+    return cells
+
+
+def _full_lane_vs_oracle(plan, lane, lat, mtr, utr, alpha, beta, c):
+    """Every cell of ``lane`` of the plan's last pass against the oracle's memory-lean run
+    of that one lane over the whole lattice (oracle.cv_lane: the kpo_cv recurrence, train
+    counts only, 12 B/cell; the k-mers' train counts = all data - the lane's fold), read
+    back in chunks of 2^27 cells.  Returns the number of cells compared."""
+    from oracle import oracle as O
+    from tests.fixtures import bits_equal
+    ref = O.cv_lane(lat.gp, _kmer_cells(lat), mtr, utr, alpha, beta, c, 32, threads=_threads())
+    n = ref.size
+    assert n == plan.info["npat"]
+    step = 1 << 27
+    for i0 in range(0, n, step):
+        i1 = min(n, i0 + step)
+        got = plan.gather_cells(lane, np.arange(i0, i1, dtype=np.uint64))
+        if not bits_equal(got, ref[i0:i1]):
+            bad = np.nonzero((got.view(np.uint32) != ref[i0:i1].view(np.uint32)) &
+                             ~(np.isnan(got) & np.isnan(ref[i0:i1])))[0]
+            raise AssertionError(f"lane {lane}: {bad.size} cells of [{i0}, {i1}) differ, first {i0 + int(bad[0])} "
+                                 f"({lat.pattern(i0 + int(bad[0]))}): {got[bad[0]]!r} vs {ref[i0 + bad[0]]!r}")
+    del ref
+    return n
+
+
+def _grid_cv_order(mtr, utr, alphas, pens, nf):
+    """The CV driver's groups (alpha-major, folds in shard.fold_order, CV :138-145 of the
+    drop-in), with float betas."""
+    from kmerpapa_amd.score_utils import get_betas
+    from kmerpapa_amd.shard import fold_order
+    grid = []
+    for a in alphas:
+        betas = get_betas(a, mtr, utr)
+        grid += [(f, a, float(betas[f]), list(pens)) for f in fold_order(nf)]
+    return grid
+
+
+@pytest.mark.timeout(1500)
+def test_9mer_8rank_shares_pinned_full_size(cv_split):
+    """BASELINE configs[3] as the 8-GPU job runs it: each rank's share of the 5x5x5 grid as
+    its own passes ([5], [5], [5 + 1] or [5], [5], [5]), one rank after the other on this
+    GPU.  Ranks 0, 4 and 7 (a [5 + 1] pass of two folds, one of two alphas of the same fold,
+    a 15-lane share): every lane's root train / test and partition re-derived on the host
+    with every split candidate of every tree node re-derived one level down (47 lanes); rank 0's packed odd
+    lane (another fold's single lane beside a 5-lane group) equal to the oracle in all
+    7.69e9 cells; the eight ranks' roots unsharded equal the one-GPU job's bit for bit."""
+    from kmerpapa_amd import engine, shard
+    from oracle import treecheck as T
+    sp = cv_split
+    grid = _grid_cv_order(sp["mtr"], sp["utr"], ALPHAS9, PENS9, 5)
+    dev = engine.visible_devices()[0]
+    plan = engine.get_plan(dev, GEN_PAT, 0)
+    plan.set_counts(sp["Mk"], sp["Uk"])
+    width = plan.info["lanes_per_workgroup"]
+    assert width == 5
+    if len(_GRID9) < 125:  # (the 125-lane test did not run first) the one-GPU job's passes
+        rt, re, nl = engine.run_groups(GEN_PAT, sp["Mk"], sp["Uk"], grid, devices=[dev])
+        lane = 0
+        for f, a, b, pens in grid:
+            for c in pens:
+                _GRID9[(f, a, c)] = (rt[lane], re[lane], nl[lane])
+                lane += 1
+    lat = T.Lattice(GEN_PAT)
+    Mk, Uk = sp["Mk"].astype(np.int64), sp["Uk"].astype(np.int64)
+    Mall, Uall = Mk.sum(axis=1), Uk.sum(axis=1)
+    stats, parts, full_cells = {}, [], 0
+    for r in range(8):
+        mine = shard.rank_groups(grid, r, 8)
+        passes, order = engine.plan_passes(mine, engine.pass_cap(mine, plan.require_lanes(), width), width)
+        shape = [[len(g[3]) for g in pas] for pas in passes]
+        if r == 0:
+            assert shape == [[5], [5], [5, 1]] and len({g[0] for g in passes[-1]}) == 2, shape
+        if r == 4:
+            assert shape == [[5], [5], [5, 1]] and len({g[0] for g in passes[-1]}) == 1, shape
+        if r == 7:
+            assert shape == [[5], [5], [5]], shape
+        outs = []
+        for pas in passes:
+            rt, re, nl = plan.run(pas)
+            outs.append((rt, re, nl))
+            if r in (0, 4, 7):
+                nlanes = sum(len(g[3]) for g in pas)
+                _tree_check_pass(plan, lat, pas, Mk, Uk, rt, re, nl, offtree=range(nlanes), stats=stats)
+            if r == 0 and len(pas) == 2:  # the packed two-fold pass: its odd lane over the whole lattice
+                f, a, b, pens = pas[1]
+                full_cells += _full_lane_vs_oracle(plan, 5, lat, Mall - Mk[:, f], Uall - Uk[:, f], a, b, pens[0])
+        parts.append(tuple(engine.unpermute_lanes(order, np.concatenate([o[i] for o in outs])) for i in range(3)))
+    got = [shard.unshard(grid, 8, [p[i] for p in parts]) for i in range(3)]
+    want = [np.array([_GRID9[(f, a, c)][i] for f, a, b, pens in grid for c in pens]) for i in range(3)]
+    for g, w in zip(got[:2], want[:2]):
+        assert np.array_equal(np.asarray(g, np.float32).view(np.uint32), np.asarray(w, np.float32).view(np.uint32))
+    assert np.array_equal(np.asarray(got[2], np.uint64), np.asarray(want[2], np.uint64))
+    assert stats["lanes"] == 47 and stats["offtree_lanes"] == 47 and full_cells == plan.info["npat"]
+    print(f"9-mer 8 ranks: 125 lanes unsharded = one-GPU roots; ranks 0, 4, 7: {stats['lanes']} lanes, "
+          f"{stats['nodes']} tree nodes, {stats['candidates']} split candidates re-derived; "
+          f"{full_cells} cells of the packed odd lane = oracle")
+
+
+@pytest.mark.timeout(1500)
+def test_11mer_8rank_share_mid_fold_pinned_full_size():
+    """BASELINE configs[4] (ANNNNMNNNNA, 10 folds, 7x7 grid = 490 lanes) as the 8-GPU job
+    cuts it: rank 1's share starts in the middle of a (alpha, fold) group and spans two
+    alphas, so its passes pack pieces of different folds.  Every lane's root and partition
+    is re-derived on the host (with every split candidate one level down on every fourth
+    lane), a packed lane is compared with the oracle over the whole lattice, and the share's
+    roots equal the same lanes run as the one-GPU job runs their groups."""
+    from kmerpapa_amd import engine, shard
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality
+    from oracle import treecheck as T
+    import bench
+    gp, nf = "ANNNNMNNNNA", 10
+    kmers, M, U = bench.synthetic_counts(gp, seed=9)
+    ctx = {k: (int(m), int(u)) for k, m, u in zip(kmers, M, U)}
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(1), np.uint32)
+    Mk, Uk = engine.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), np.uint32)
+    ms, us = Mf.sum(axis=0, dtype=np.uint64), Uf.sum(axis=0, dtype=np.uint64)
+    grid = _grid_cv_order(ms.sum() - ms, us.sum() - us, ALPHAS11, PENS11, nf)
+    rank = 1
+    ids = shard.assign_lanes(grid, 8)[rank]
+    assert ids[0] % len(PENS11) != 0  # starts mid-group
+    mine = shard.rank_groups(grid, rank, 8)
+    assert len({g[1] for g in mine}) == 2
+    engine.release_all()
+    dev = engine.visible_devices()[0]
+    plan = engine.get_plan(dev, gp, 0)
+    plan.set_counts(Mk, Uk)
+    width = plan.info["lanes_per_workgroup"]
+    passes, order = engine.plan_passes(mine, engine.pass_cap(mine, plan.require_lanes(), width), width)
+    assert any(len({g[0] for g in pas}) == 2 for pas in passes)  # packed pieces of two folds
+    lat = T.Lattice(gp)
+    Mk64, Uk64 = Mk.astype(np.int64), Uk.astype(np.int64)
+    Mall, Uall = Mk64.sum(axis=1), Uk64.sum(axis=1)
+    stats, outs, full_cells, k = {}, [], 0, 0
+    for pas in passes:
+        rt, re, nl = plan.run(pas)
+        outs.append((rt, re, nl))
+        nlanes = sum(len(g[3]) for g in pas)
+        _tree_check_pass(plan, lat, pas, Mk64, Uk64, rt, re, nl,
+                         offtree=[j for j in range(nlanes) if (k + j) % 4 == 0], stats=stats)
+        if not full_cells and len({g[0] for g in pas}) == 2:  # first packed pass: its last lane
+            f, a, b, pens = pas[-1]
+            full_cells = _full_lane_vs_oracle(plan, nlanes - 1, lat, Mall - Mk64[:, f], Uall - Uk64[:, f], a, b,
+                                              pens[-1])
+        k += nlanes
+    share = [np.concatenate([o[i] for o in outs]) for i in range(3)]
+    share = [engine.unpermute_lanes(order, x) for x in share]
+    # the one-GPU job's passes over the groups this share touches
+    touched = sorted({(g[0], g[1]) for g in mine})
+    groups1 = [g for g in grid if (g[0], g[1]) in touched]
+    p1, o1 = engine.plan_passes(groups1, engine.pass_cap(groups1, plan.require_lanes(), width), width)
+    res1 = [plan.run(pas) for pas in p1]
+    one = [engine.unpermute_lanes(o1, np.concatenate([x[i] for x in res1])) for i in range(3)]
+    key1 = {(f, a, c): j for j, (f, a, c) in enumerate((f, a, c) for f, a, b, pens in groups1 for c in pens)}
+    sel = [key1[(f, a, c)] for f, a, b, pens in mine for c in pens]
+    for i in range(2):
+        assert np.array_equal(np.asarray(share[i], np.float32).view(np.uint32),
+                              np.asarray(one[i], np.float32)[sel].view(np.uint32))
+    assert np.array_equal(np.asarray(share[2], np.uint64), np.asarray(one[2], np.uint64)[sel])
+    assert stats["lanes"] == len(ids) and stats["offtree_lanes"] >= 10 and full_cells == plan.info["npat"]
+    print(f"11-mer rank 1 of 8: {stats['lanes']} lanes in {len(passes)} passes = one-GPU roots; "
+          f"{stats['nodes']} tree nodes, {stats['candidates']} split candidates ({stats['offtree_lanes']} lanes) "
+          f"re-derived; {full_cells} cells of a packed lane = oracle")
     engine.release_all()

@@ -95,3 +95,89 @@ def test_treecheck_catches_a_changed_child(grid5):
         with pytest.raises(T.TreeMismatch):
             T.rederive(lat, lambda cells: t[cells.astype(np.int64)], Mk.sum(axis=1) - Mk[:, 0],
                        Uk.sum(axis=1) - Uk[:, 0], Mk[:, 0], Uk[:, 0], 1.0, float(betas[0]), 5.0)
+
+
+def _lane0(grid5, alpha=1.0, penalty=5.0):
+    from kmerpapa_amd.score_utils import get_betas
+    gp, contexts, Mf, Uf = grid5
+    lat = T.Lattice(gp)
+    idx = _kmer_index(lat, contexts)
+    Mk = np.zeros((lat.n_kmers, 5), np.int64)
+    Uk = np.zeros((lat.n_kmers, 5), np.int64)
+    Mk[idx], Uk[idx] = Mf, Uf
+    ms, us = Mf.sum(axis=0), Uf.sum(axis=0)
+    betas = get_betas(alpha, ms.sum() - ms, us.sum() - us)
+    ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, penalty, 32)
+    args = (Mk.sum(axis=1) - Mk[:, 0], Uk.sum(axis=1) - Uk[:, 0], Mk[:, 0], Uk[:, 0], alpha, float(betas[0]), penalty)
+    mtr = (ref["M"].sum(axis=1) - ref["M"][:, 0]).astype(np.int64)  # every cell's train counts
+    utr = (ref["U"].sum(axis=1) - ref["U"][:, 0]).astype(np.int64)
+    return lat, ref["score"][:, 0].copy(), args, mtr, utr
+
+
+def _root_candidates(lat):
+    dig = lat.digits(lat.root)
+    out = []
+    for i, d in enumerate(dig):
+        base = lat.root - d * lat.cw[i]
+        for pa, pb in lat.pairs[i][d]:
+            out.append((base + pa * lat.cw[i], base + pb * lat.cw[i]))
+    return out
+
+
+@pytest.mark.parametrize("alpha,penalty", [(1.0, 5.0), (0.0, 2.0)])
+def test_local_values_reproduce_every_cell(grid5, alpha, penalty):
+    """The one-level re-derivation (local_values) of EVERY cell of the lattice from the
+    oracle's stored scores and train counts gives the oracle's own value bit for bit
+    (alpha = 0: empty k-mers give p = 0/0, NaN encodings included)."""
+    from tests.fixtures import bits_equal
+    lat, s, (mtr_k, utr_k, _, _, a, b, c), mtr, utr = _lane0(grid5, alpha, penalty)
+    cells = np.arange(s.size)
+    got = T.local_values(lat, cells, mtr, utr, lambda x: s[x.astype(np.int64)], a, b, c)
+    assert bits_equal(got, s)
+
+
+def test_offtree_too_high_candidate_caught(grid5):
+    """A split candidate of the root that does NOT win, stored one ulp too high: the root's
+    first minimum is unchanged, so the on-tree walk alone passes; the candidate's own
+    re-derivation (offtree) fails."""
+    lat, s, args, _, _ = _lane0(grid5)
+    r = T.rederive(lat, lambda x: s[x.astype(np.int64)], *args)
+    assert r["candidates"] > 2 * r["nodes"]
+    left = set(int(x) for x in np.asarray(r["leaves"]))
+    best = min(np.float32(s[c1] + s[c2]) for c1, c2 in _root_candidates(lat))
+    loser = next(c1 for c1, c2 in _root_candidates(lat)
+                 if np.float32(s[c1] + s[c2]) > best and c1 not in left)
+    t = s.copy()
+    t[loser] = np.nextafter(t[loser], np.float32(np.inf))
+    g = lambda x: t[x.astype(np.int64)]  # noqa: E731
+    T.rederive(lat, g, *args, offtree=False)
+    with pytest.raises(T.TreeMismatch, match="split candidate"):
+        T.rederive(lat, g, *args)
+
+
+def test_offtree_flipped_argmin_caught(grid5):
+    """The verdict's case: the root's WINNING child stored too high, and every cell above it
+    recomputed consistently from that value (as a sweep that read the wrong value would
+    have): the root's argmin flips to a worse split and the on-tree walk reproduces the
+    flipped tree bit for bit; the off-tree re-derivation of the too-high child fails."""
+    lat, s, args, mtr, utr = _lane0(grid5)
+    r0 = T.rederive(lat, lambda x: s[x.astype(np.int64)], *args)
+    sums = [(np.float32(s[c1] + s[c2]), c1) for c1, c2 in _root_candidates(lat)]
+    best = min(v for v, _ in sums)
+    win = next(c1 for v, c1 in sums if v == best)
+    t = s.copy()
+    t[win] = t[win] + np.float32(1e4)
+    lev = lat.digit_array(np.arange(s.size))
+    lvl = np.zeros(s.size, np.int64)
+    for i, g in enumerate(lat.gp):
+        lv = np.array([len(T.IUPAC[x]) - 1 for x in O._PERM[g]])
+        lvl += lv[lev[:, i]]
+    a, b, c = args[4:]
+    for L in range(int(lvl[win]) + 1, int(lvl.max()) + 1):
+        cells = np.nonzero(lvl == L)[0]
+        t[cells] = T.local_values(lat, cells, mtr[cells], utr[cells], lambda x: t[x.astype(np.int64)], a, b, c)
+    g = lambda x: t[x.astype(np.int64)]  # noqa: E731
+    r1 = T.rederive(lat, g, *args, offtree=False)  # consistent above the bad cell: passes
+    assert not np.array_equal(r1["leaves"], r0["leaves"])  # ... with a different tree
+    with pytest.raises(T.TreeMismatch, match="split candidate"):
+        T.rederive(lat, g, *args)
