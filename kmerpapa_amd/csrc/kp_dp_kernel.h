@@ -49,12 +49,14 @@ struct kp_dp_params {
                                           // not vector loads whose waits stalled every level's start)
     uint32_t ptab_entries;     // separable count table entries (kp_plan.h)
     uint32_t pscratch_entries; // largest intermediate table of its build
+    uint32_t wscratch_entries; // largest table before the last step (kp_dp_ws.h's build buffers)
     int remap;  // block -> XCD mapping: G > 1 = runs of G list entries per XCD (default 40),
                 // 1 = XCD-contiguous (7 % slower), 0 = hardware round-robin
     int lanesplit;  // split a cell's lanes over threads on narrow levels (KP_LANE_SPLIT=0 disables)
     int ntstore;    // 1 = score rows stored non-temporally (default; KP_NT_STORE=0 for plain stores)
     uint32_t ntmask;  // high positions whose child rows are loaded non-temporally (bit i = high position i)
     unsigned long long *stamps;  // diagnostic build only (-DKP_STAMPS): per-phase cycle sums
+    uint32_t *werr;              // kp_dp_ws_kernel: set when a hand-over wait timed out (the pass fails)
     int exact;      // 1 = every cell's single term from the C library's logs (KP_EXACT_LOGS=1)
     int dbg;  // -DKP_ABLATION builds only (KP_DEBUG_SKIP, wrong results; always 0 otherwise): 1 = skip gather, 2 = skip level phase,
               // 4 = skip logs, 8 = skip low split scan, 16 = no level barrier

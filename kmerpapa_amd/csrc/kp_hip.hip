@@ -42,6 +42,7 @@
 #include "kp_allk.h"
 #include "kp_core.h"
 #include "kp_dp_kernel.h"
+#include "kp_dp_ws.h"
 #include "kp_folds.h"
 #include "kp_io.h"
 #include "kp_out.h"
@@ -457,6 +458,7 @@ struct kp_ctx {
     hipStream_t side[KP_SIDE_STREAMS] = {nullptr, nullptr, nullptr};
     hipEvent_t side_ev[KP_SIDE_STREAMS] = {nullptr, nullptr, nullptr};
     size_t lds_max = 65536;
+    int cus = 256;  // compute units (the persistent sweep's grid)
 };
 
 struct kp_plan {
@@ -501,6 +503,9 @@ struct kp_plan {
     kp_group_dev *d_groups = nullptr;
     uint32_t *d_lanegrp = nullptr;
     float *d_rtrain = nullptr, *d_rtest = nullptr;
+    kp_dp_params *d_wsp = nullptr;  // launch parameters of the pass's kp_dp_ws_kernel launches (device copy)
+    size_t wsp_cap = 0;
+    uint32_t *d_werr = nullptr;  // kp_dp_ws_kernel's error word (a hand-over wait timed out)
     uint64_t *d_nleaves = nullptr;
     uint32_t *d_bad = nullptr;
     uint32_t *d_cnt = nullptr;
@@ -590,6 +595,8 @@ int kp_create(int device, kp_ctx **out) {
     int lds = 0;
     if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess && lds > 0)
         c->lds_max = (size_t)lds;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) c->cus = cus;
     *out = c;
     return KP_OK;
 }
@@ -729,6 +736,8 @@ void kp_plan_destroy(kp_plan *p) {
                     p->d_leaves};
     if (p->cstream) (void)hipStreamSynchronize(p->cstream);
     for (void *b : bufs) dfree(b);
+    dfree(p->d_wsp);
+    dfree(p->d_werr);
     dfree(p->d_stage);
     if (p->h_stage) (void)hipHostFree(p->h_stage);
     if (p->stage_ev) (void)hipEventDestroy(p->stage_ev);
@@ -1066,6 +1075,70 @@ static int launch_dp_nl(int nl, bool mix, hipStream_t c, const kp_dp_params &P, 
     return fail(KP_E_ARG, "lanes per workgroup must be 1..8");
 }
 
+// The wave-specialised persistent sweep (kp_dp_ws.h) for 1-lane device groups above high
+// level 0, with KP_WS=1 (A/B; off by default until it measures faster).
+static bool ws_enabled() {
+    const char *e = getenv("KP_WS");
+    return e && atoi(e) != 0;
+}
+
+// its build buffers: the largest count table before the last step (T_0 .. T_{t-2})
+static uint32_t ws_scratch_entries(const kp::host_plan &hp) {
+    const kp_geom &g = hp.g;
+    uint64_t R = 1, mx = 1;
+    for (int s = 0; s + 1 < g.t; ++s) {
+        uint64_t nn = 1;
+        for (int i = s; i < g.t; ++i) nn *= g.n[i];
+        mx = std::max<uint64_t>(mx, R * nn);
+        R *= g.r[s];
+    }
+    return (uint32_t)mx;
+}
+
+// dynamic LDS of kp_dp_ws_kernel (carve order as in the kernel)
+static size_t ws_lds_bytes(const kp::host_plan &hp, size_t ct_bytes) {
+    const kp_geom &g = hp.g;
+    const size_t ptab = (((size_t)hp.ptab_entries * 2 + 3) & ~(size_t)3) * ct_bytes;
+    const size_t scr = (((size_t)ws_scratch_entries(hp) * 2 + 3) & ~(size_t)3) * ct_bytes;
+    return 2 * (size_t)KP_WS_BASE1 + 2 * ptab + 2 * scr + (size_t)(g.kh * 7 + 1) * sizeof(kp_hpair) +
+           (((size_t)g.t * 16 + 15) & ~(size_t)15) + sizeof(kp_ws_sync);
+}
+
+// can this launch (one high level of a class of nl-lane device groups) run on the
+// wave-specialised sweep?  Its slots need a level per count-table step and a gather slot,
+// its row buffers a block of <= 4128 floats, its consumers every level's cells
+static bool ws_fits(const kp::host_plan &hp, const kp_dp_params &P, int nl, bool mix, size_t ct_bytes,
+                    size_t lds_max) {
+    if (!ws_enabled() || nl != 1 || mix || P.H == 0 || !P.T.hpd || !P.lanesplit) return false;
+    const kp_geom &g = hp.g;
+    const int L = hp.lmax + 1;
+    if (L < 2 || g.t > L || (size_t)g.Bpad * 4 > KP_WS_BASE1) return false;
+    for (int l = 0; l <= hp.lmax; ++l)
+        if (hp.loff[l + 1] - hp.loff[l] > KP_WS_CW * 64 * KP_IPT) return false;
+    return ws_lds_bytes(hp, ct_bytes) <= std::min<size_t>(lds_max, 80u * 1024u);  // two workgroups per CU
+}
+
+template <typename CT>
+static int launch_ws(hipStream_t st, const kp_dp_params *dP, unsigned nb, unsigned ngroups, int cus, size_t lds) {
+    static std::atomic<bool> checked{false};
+    if (!checked.load(std::memory_order_relaxed)) {  // its scan reads the row buffers at fixed LDS addresses
+        hipFuncAttributes fa;
+        KP_HIP(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(&kp_dp_ws_kernel<CT, 1>)));
+        if (fa.sharedSizeBytes != 0) return fail(KP_E_HIP, "kp_dp_ws_kernel has static LDS");
+        checked.store(true, std::memory_order_relaxed);
+    }
+    if (lds > 65536)
+        KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_ws_kernel<CT, 1>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    // persistent: two workgroups per CU over the class's device groups, a multiple of 8
+    // workgroups per group (one XCD per workgroup's blocks)
+    unsigned wmax = (unsigned)std::max(8, (2 * cus / (int)std::max(1u, ngroups)) & ~7);
+    const unsigned W = std::min(nb, wmax);
+    hipLaunchKernelGGL((kp_dp_ws_kernel<CT, 1>), dim3(W, ngroups), dim3(KP_WS_THREADS), lds, st, dP, nb);
+    KP_HIP(hipGetLastError());
+    return KP_OK;
+}
+
 static int dp_threads() {
     const char *e = getenv("KP_DP_THREADS");
     int v = e ? atoi(e) : 512;
@@ -1351,6 +1424,7 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         if (hp.loff[l + 1] <= hp.loff[l]) return fail(KP_E_ARG, "empty low level");
     P.ptab_entries = hp.ptab_entries;
     P.pscratch_entries = hp.pscratch_entries;
+    P.wscratch_entries = ws_scratch_entries(hp);
 #ifdef KP_ABLATION
     // timing-ablation build only (make ablation -> libkmerpapa_hip_ablation.so): phases
     // skipped by KP_DEBUG_SKIP give wrong scores, so the pass reports KP_E_STATE below
@@ -1414,6 +1488,45 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         classes.emplace_back(i, j);
         i = j;
     }
+    // the launches that run on the wave-specialised sweep (kp_dp_ws.h) read their parameters
+    // from device memory: all of the pass's, uploaded once before the first launch
+    auto launch_params = [&](size_t i, int H) {
+        kp_dp_params Q = P;
+        Q.hbase = hp.hoff[H];
+        Q.H = H;
+        Q.groups = p->d_groups + i;
+        Q.ntmask = ntmask_h[H];
+        return Q;
+    };
+    if (!p->d_werr) KP_HIP(dmalloc(&p->d_werr, sizeof(uint32_t)));
+    KP_HIP(hipMemsetAsync(p->d_werr, 0, sizeof(uint32_t), c->stream));
+    P.werr = p->d_werr;
+    std::vector<kp_dp_params> wsq;
+    std::vector<int> wsat(classes.size() * (size_t)(hp.hmax + 1), -1);
+    for (size_t q = 0; q < classes.size(); ++q) {
+        const size_t i = classes[q].first, j = classes[q].second;
+        bool mix = false;
+        for (size_t q2 = i; q2 < j; ++q2) mix = mix || dg[q2].nl2 > 0;
+        for (int H = 0; H <= hp.hmax; ++H) {
+            if (hp.hoff[H + 1] == hp.hoff[H]) continue;
+            const kp_dp_params Q = launch_params(i, H);
+            if (ws_fits(hp, Q, dg[i].nl, mix, sizeof(CT), c->lds_max)) {
+                wsat[q * (hp.hmax + 1) + H] = (int)wsq.size();
+                wsq.push_back(Q);
+            }
+        }
+    }
+    if (!wsq.empty()) {
+        if (wsq.size() > p->wsp_cap) {
+            dfree(p->d_wsp);
+            p->d_wsp = nullptr;
+            p->wsp_cap = 0;
+            KP_HIP(dmalloc(&p->d_wsp, wsq.size() * sizeof(kp_dp_params)));
+            p->wsp_cap = wsq.size();
+        }
+        KP_HIP(hipMemcpyAsync(p->d_wsp, wsq.data(), wsq.size() * sizeof(kp_dp_params), hipMemcpyHostToDevice,
+                              c->stream));
+    }
     // KP_CLASS_STREAMS=1 runs the classes concurrently.  Off by default: measured on one
     // MI355X, 9-mer passes of 4+3 lanes (one 7-penalty group) 620 -> 603 ms and 5+1 / 4+2
     // (two groups) -0.5 %, but the 11-mer step (4+3 lanes, ANNNNMNNNNA) 606 -> 627 ms
@@ -1452,7 +1565,13 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
             }
             bool mix = false;
             for (size_t q2 = i; q2 < j; ++q2) mix = mix || dg[q2].nl2 > 0;
-            int rc = launch_dp_nl<CT>(dg[i].nl, mix, st, Q, (unsigned)nb, (unsigned)(j - i), threads, lds);
+            int rc;
+            const int wi = wsat[q * (hp.hmax + 1) + H];
+            if (wi >= 0)
+                rc = launch_ws<CT>(st, p->d_wsp + wi, (unsigned)nb, (unsigned)(j - i), c->cus,
+                                   ws_lds_bytes(hp, sizeof(CT)));
+            else
+                rc = launch_dp_nl<CT>(dg[i].nl, mix, st, Q, (unsigned)nb, (unsigned)(j - i), threads, lds);
             if (rc) return rc;
             if (timed) KP_HIP(hipEventRecord(p->lev[2 * launches + 1], st));
             ++launches;
@@ -1510,7 +1629,10 @@ static int run_pass(kp_plan *p, const kp_group *groups, int n_groups, float *roo
         KP_HIP(hipMemcpyAsync(nlv.data(), p->d_nleaves, Ltot * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
         KP_HIP(hipMemcpyAsync(bad.data(), p->d_bad, Ltot * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     }
+    uint32_t werr = 0;
+    KP_HIP(hipMemcpyAsync(&werr, p->d_werr, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
     KP_HIP(hipStreamSynchronize(c->stream));
+    if (werr) return fail(KP_E_HIP, "kp_dp_ws_kernel: a hand-over wait timed out (results invalid)");
     float dp_ms = 0, bt_ms = 0;
     KP_HIP(hipEventElapsedTime(&dp_ms, c->ev[0], c->ev[1]));
 #ifdef KP_STAMPS

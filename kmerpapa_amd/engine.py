@@ -144,7 +144,7 @@ def _ptr(a):
 # launch knobs read by kp_hip.hip (every setting gives the same scores; they change timing)
 LAUNCH_KNOBS = ("KP_DP_THREADS", "KP_LANES_PER_WG", "KP_XCD_REMAP", "KP_LANE_SPLIT", "KP_NT_STORE", "KP_NT_SLOW",
                 "KP_BLOCK_PERM", "KP_BLOCK_ORDER", "KP_BLOCK_TILE", "KP_LOW_ORDER", "KP_EXACT_LOGS",
-               "KP_CLASS_STREAMS", "KP_NT_SLOW_H", "KP_LDS_BUDGET", "KP_WIDE_SPLIT", "KP_HPD")
+               "KP_CLASS_STREAMS", "KP_NT_SLOW_H", "KP_LDS_BUDGET", "KP_WIDE_SPLIT", "KP_HPD", "KP_WS")
 
 
 _toolchain = None

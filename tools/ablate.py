@@ -3,7 +3,8 @@ skipped.  Needs the timing-ablation build (make -C kmerpapa_amd/csrc ablation) a
 KMERPAPA_LIB=kmerpapa_amd/libkmerpapa_hip_ablation.so; every ablated pass returns
 KP_E_STATE (its numbers are invalid) after recording its timings.
 usage: python tools/ablate.py SKIP [SKIP ...]   (KP_DEBUG_SKIP bit sets, 0 = full pass;
-  ABLATE_LANES=n: a pass of the group's first n penalties, default 5)
+  ABLATE_LANES=n: a pass of the group's first n penalties, default 5; ABLATE_PATTERN=gen_pat:
+  another lattice, default NNNNMNNNN)
   1 = no gather, 2 = no level phase, 4 = no float64 logs, 8 = no low split scan,
   16 = no level barriers"""
 import json
@@ -14,10 +15,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from kmerpapa_amd import engine  # noqa: E402
 
-prep = bench.prepare("NNNNMNNNN")
-plan = engine.get_plan(0, "NNNNMNNNN")
+GP = os.environ.get("ABLATE_PATTERN", "NNNNMNNNN")
+prep = bench.prepare(GP)
+plan = engine.get_plan(0, GP)
 plan.set_counts(prep["Mk"], prep["Uk"])
-plan.reserve(5)
+plan.reserve(int(os.environ.get("ABLATE_LANES", "5")))
 g = prep["groups"][0]
 g = (g[0], g[1], g[2], list(g[3])[:int(os.environ.get("ABLATE_LANES", "5"))])
 for skip in sys.argv[1:] or ["0"]:
