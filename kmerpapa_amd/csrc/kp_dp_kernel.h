@@ -85,7 +85,9 @@ struct kp_dp_params {
 #define KP_SKIP(P, bit) false
 #endif
 
+#ifndef KP_IPT
 #define KP_IPT 2  // low cells per thread per level (host checks level sizes)
+#endif
 // count-table reads of a cell all in flight at once (kp_ptab_counts ALL): A/B knob, see
 // profiles/r03/experiments/count_reads_ab.txt
 #ifndef KP_PTAB_ALL

@@ -467,7 +467,8 @@ kp_dp_ws_kernel(const kp_dp_params *Pg, uint32_t nb) {
                 const kp_cnt kpre = {(uint64_t)k0 - kte_m, (uint64_t)k1 - kte_u, 0, 0};
                 kp_ws_count_step<CT>(g, 0, K, pq, fold, lm, bufA, bufB, pptab, ptid, NPROD, kpre);
                 kp_ws_role_barrier(&sy->pbar, KP_WS_PW, pgen, sy, werr);  // hp, T_0
-                kp_ws_gather<NL, KP_WS_NI, KP_WS_PU>(P, hp, 0, np, nnt, true, true, lane0, pst, ptid, NPROD);
+                if (!KP_SKIP(P, 1))  // (timing-ablation builds only: skip the gather)
+                    kp_ws_gather<NL, KP_WS_NI, KP_WS_PU>(P, hp, 0, np, nnt, true, true, lane0, pst, ptid, NPROD);
                 for (int s = 1; s < g.t; ++s) {
                     kp_ws_count_step<CT>(g, s, K, pq, fold, lm, bufA, bufB, pptab, ptid, NPROD, kp_cnt{});
                     if (s + 1 < g.t) kp_ws_role_barrier(&sy->pbar, KP_WS_PW, pgen, sy, werr);
@@ -492,7 +493,8 @@ kp_dp_ws_kernel(const kp_dp_params *Pg, uint32_t nb) {
         for (int i = 0; i < nblk; ++i) {
             kp_ws_wait(&sy->full, (uint32_t)(i + 1) * KP_WS_PW, sy, werr);
             const CT *cptab = ptabs + (size_t)(i & 1) * ptab_elems;
-            if (i & 1)
+            if (KP_SKIP(P0, 2)) {  // (timing-ablation builds only: no level phase)
+            } else if (i & 1)
                 kp_ws_levels<CT, NL, KP_WS_BASE1>(PP, lmax, lm, cptab, pen, alpha, beta, exact, ctid, ncons, cur, cgen,
                                                   sy, werr);
             else

@@ -1130,9 +1130,12 @@ static int launch_ws(hipStream_t st, const kp_dp_params *dP, unsigned nb, unsign
     if (lds > 65536)
         KP_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&kp_dp_ws_kernel<CT, 1>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    // persistent: two workgroups per CU over the class's device groups, a multiple of 8
-    // workgroups per group (one XCD per workgroup's blocks)
-    unsigned wmax = (unsigned)std::max(8, (2 * cus / (int)std::max(1u, ngroups)) & ~7);
+    // persistent: as many workgroups as are resident at once (waves per SIMD x 4 SIMDs per CU
+    // over the workgroup's waves; LDS), shared by the class's device groups, a multiple of 8
+    // per group (one XCD per workgroup's blocks)
+    const int per_cu = std::max(1, std::min<int>((4 * KP_WS_WAVES) / (KP_WS_THREADS / 64),
+                                                 (int)((160u * 1024u) / std::max<size_t>(lds, 1))));
+    unsigned wmax = (unsigned)std::max(8, (per_cu * cus / (int)std::max(1u, ngroups)) & ~7);
     const unsigned W = std::min(nb, wmax);
     hipLaunchKernelGGL((kp_dp_ws_kernel<CT, 1>), dim3(W, ngroups), dim3(KP_WS_THREADS), lds, st, dP, nb);
     KP_HIP(hipGetLastError());

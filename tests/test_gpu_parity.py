@@ -461,6 +461,53 @@ def test_lanes_per_workgroup_vs_oracle(eng, per_wg, monkeypatch):
     plan.close()
 
 
+@pytest.mark.parametrize("gp,max_block,itype,exact", [("NNMNN", 0, np.uint32, 0), ("NNMNN", 0, np.uint32, 1),
+                                                      ("RNNNS", 64, np.uint32, 0), ("NNNMN", 0, np.uint64, 0)])
+def test_persistent_1lane_sweep_vs_oracle(eng, monkeypatch, gp, max_block, itype, exact):
+    """The opt-in persistent wave-specialised sweep for 1-lane groups (kp_dp_ws.h, KP_WS=1:
+    producer waves gather block i + 1 while consumer waves run block i's levels, LDS-counter
+    hand-over): every device group cut to one lane (KP_LANES_PER_WG=1), so every launch above
+    high level 0 runs on it; every cell of every lane equals the oracle, with 32- and 64-bit
+    counts, and in KP_EXACT_LOGS mode."""
+    from kmerpapa_amd.CV_tools import fold_tables
+    from kmerpapa_amd.pattern_utils import generality, matches
+    from oracle import oracle as O
+    monkeypatch.setenv("KP_WS", "1")
+    monkeypatch.setenv("KP_LANES_PER_WG", "1")
+    monkeypatch.setenv("KP_EXACT_LOGS", str(exact))
+    rng = np.random.RandomState(len(gp) + max_block)
+    scale = 1e7 if itype == np.uint64 else 2e4
+    ctx = {}
+    for k in matches(gp):
+        bg = int(rng.poisson(scale * rng.lognormal(0, 0.5)))
+        ctx[k] = (int(rng.binomial(bg, 0.01 * rng.lognormal(0, 0.4))), bg)
+    if itype == np.uint64:
+        assert sum(m + u for m, u in ctx.values()) > 2 ** 32
+    nf = 3
+    contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(3), itype)
+    Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), itype)
+    alpha = 0.5
+    tot_m = Mf.sum(axis=0).astype(np.uint64)
+    tot_u = Uf.sum(axis=0).astype(np.uint64)
+    mtr = tot_m.sum() - tot_m
+    utr = tot_u.sum() - tot_u
+    betas = (alpha * (1.0 - mtr / (mtr + utr))) / (mtr / (mtr + utr))
+    pens = [2.0, 5.0]
+    plan = eng.Plan(eng.get_device(0), gp, max_block)
+    plan.set_counts(Mk, Uk)
+    assert plan.info["high_levels"] > 2
+    rt, re, _ = plan.run([(f, alpha, float(betas[f]), pens) for f in range(nf)])
+    bits = 64 if itype == np.uint64 else 32
+    for pi, c in enumerate(pens):
+        ref = O.cv_pass(gp, contexts, Mf, Uf, alpha, betas, c, bits)
+        for f in range(nf):
+            lane = f * len(pens) + pi
+            score, _ = plan.dump_lane(lane)
+            assert bits_equal(score, ref["score"][:, f]), (gp, c, f)
+            assert bits_equal(rt[lane], ref["root_train"][f]) and bits_equal(re[lane], ref["root_test"][f])
+    plan.close()
+
+
 # (lane counts of consecutive same-fold groups with alternating alphas): one mixed 5-lane
 # device group (2 + 3, 4 + 1), two mixed ones (3 + 4 + 3 -> [3 + 2], [2 + 3]), and a run that
 # would need three alphas in one workgroup (2 + 2 + 1), which stays one device group per alpha
