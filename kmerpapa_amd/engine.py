@@ -91,7 +91,9 @@ def load():
         L.kp_plan_destroy.restype = None
         L.kp_plan_get_info.argtypes = [vp, ctypes.POINTER(KPPlanInfo)]
         L.kp_plan_host.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.POINTER(KPPlanInfo)]
-        L.kp_plan_host_counts.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(KPPlanInfo)]
+        if hasattr(L, "kp_plan_host_counts"):  # (older builds loaded through KMERPAPA_LIB for A/B timing lack it)
+            L.kp_plan_host_counts.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int,
+                                              ctypes.POINTER(KPPlanInfo)]
         L.kp_block_order_check.argtypes = [ctypes.c_char_p, ctypes.c_uint32, u64p]
         L.kp_plan_block_check.argtypes = [vp, u64p]
         L.kp_kmer_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
