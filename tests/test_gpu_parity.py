@@ -461,18 +461,21 @@ def test_lanes_per_workgroup_vs_oracle(eng, per_wg, monkeypatch):
     plan.close()
 
 
-@pytest.mark.parametrize("gp,max_block,itype,exact", [("NNMNN", 0, np.uint32, 0), ("NNMNN", 0, np.uint32, 1),
-                                                      ("RNNNS", 64, np.uint32, 0), ("NNNMN", 0, np.uint64, 0)])
-def test_persistent_1lane_sweep_vs_oracle(eng, monkeypatch, gp, max_block, itype, exact):
-    """The opt-in persistent wave-specialised sweep for 1-lane groups (kp_dp_ws.h, KP_WS=1:
-    producer waves gather block i + 1 while consumer waves run block i's levels, LDS-counter
-    hand-over): every device group cut to one lane (KP_LANES_PER_WG=1), so every launch above
-    high level 0 runs on it; every cell of every lane equals the oracle, with 32- and 64-bit
-    counts, and in KP_EXACT_LOGS mode."""
+@pytest.mark.parametrize("ws", ["0", "1"])
+@pytest.mark.parametrize("gp,max_block,itype,exact,alpha", [("NNMNN", 0, np.uint32, 0, 0.5), ("NNMNN", 0, np.uint32, 1, 0.5),
+                                                            ("RNNNS", 64, np.uint32, 0, 0.5), ("NNNMN", 0, np.uint64, 0, 0.5),
+                                                            ("NNMNN", 0, np.uint32, 0, 0.0)])
+def test_1lane_sweep_vs_oracle(eng, monkeypatch, gp, max_block, itype, exact, alpha, ws):
+    """Every device group cut to one lane (KP_LANES_PER_WG=1): the 1-lane build of the sweep
+    (ws 0) and the opt-in persistent wave-specialised sweep for 1-lane groups (ws 1,
+    kp_dp_ws.h, KP_WS=1: producer waves gather block i + 1 while consumer waves run block i's
+    levels, LDS-counter hand-over; every launch above high level 0 runs on it).  Every cell of
+    every lane equals the oracle, with 32- and 64-bit counts, in KP_EXACT_LOGS mode, and with
+    alpha = 0 and k-mers of no counts (NaN k-mer cells)."""
     from kmerpapa_amd.CV_tools import fold_tables
     from kmerpapa_amd.pattern_utils import generality, matches
     from oracle import oracle as O
-    monkeypatch.setenv("KP_WS", "1")
+    monkeypatch.setenv("KP_WS", ws)
     monkeypatch.setenv("KP_LANES_PER_WG", "1")
     monkeypatch.setenv("KP_EXACT_LOGS", str(exact))
     rng = np.random.RandomState(len(gp) + max_block)
@@ -481,12 +484,13 @@ def test_persistent_1lane_sweep_vs_oracle(eng, monkeypatch, gp, max_block, itype
     for k in matches(gp):
         bg = int(rng.poisson(scale * rng.lognormal(0, 0.5)))
         ctx[k] = (int(rng.binomial(bg, 0.01 * rng.lognormal(0, 0.4))), bg)
+        if alpha == 0.0 and rng.rand() < 0.1:
+            ctx[k] = (0, 0)
     if itype == np.uint64:
         assert sum(m + u for m, u in ctx.values()) > 2 ** 32
     nf = 3
     contexts, Mf, Uf = fold_tables(ctx, nf, np.random.RandomState(3), itype)
     Mk, Uk = eng.counts_in_kmer_order(gp, contexts, Mf, Uf, generality(gp), itype)
-    alpha = 0.5
     tot_m = Mf.sum(axis=0).astype(np.uint64)
     tot_u = Uf.sum(axis=0).astype(np.uint64)
     mtr = tot_m.sum() - tot_m
