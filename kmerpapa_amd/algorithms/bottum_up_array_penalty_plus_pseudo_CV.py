@@ -70,13 +70,14 @@ def cv_roots(gen_pat, contextD, alphas, penalties, nfolds, seed, iterations, ity
         box = {}
         if prepare is not None and it == 0:
             # the GPUs' lattice tables and lane buffers are set up while the host draws the
-            # fold split (the native split releases the GIL); only lane counts matter here
+            # fold split (the native split releases the GIL); only lane counts and the
+            # counts' width matter here (a multi-GPU share depends on the width)
             shape = [(f, a, 1.0, list(penalties[c0:c0 + engine.MAX_GROUP_LANES]))
                      for a in alphas for f in fold_order(nfolds) for c0 in range(0, nc, engine.MAX_GROUP_LANES)]
 
             def _prep():
                 try:
-                    prepare(gen_pat, shape, devices=devices, max_block=max_block)
+                    prepare(gen_pat, shape, devices=devices, max_block=max_block, itype=itype)
                 except Exception as e:  # re-raised below, in the caller's thread
                     box["error"] = e
             th = threading.Thread(target=_prep)

@@ -892,7 +892,7 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0, itype=np.uint32):
     this while the host draws the fold split (CV_tools.fold_tables drops the GIL).  ``itype``
     = the counts' width to come (the shares depend on it, shard_width)."""
     devices = list(devices if devices is not None else visible_devices()[:1])
-    width = shard_width(gen_pat, itype, max_block) if len(devices) > 1 else 0
+    wg = shard_width(gen_pat, itype, max_block)  # the sweep workgroup's lanes at the counts' width
 
     errors = []
 
@@ -900,13 +900,13 @@ def prepare_groups(gen_pat, groups, devices=None, max_block=0, itype=np.uint32):
         try:
             if chunk:
                 plan = get_plan(dev, gen_pat, max_block, replica=rep)
-                width = plan.info["lanes_per_workgroup"]
-                passes, _ = plan_passes(chunk, pass_cap(chunk, plan.require_lanes(), width), width)
+                passes, _ = plan_passes(chunk, pass_cap(chunk, plan.require_lanes(), wg), wg)
                 plan.reserve(max(sum(len(g[3]) for g in pas) for pas in passes))
         except Exception as e:  # re-raised in the caller's thread
             errors.append(e)
     threads = [threading.Thread(target=prep, args=(dev, rep, chunk))
-               for dev, rep, chunk in zip(devices, _replicas(devices), _device_shares(groups, devices, width))]
+               for dev, rep, chunk in zip(devices, _replicas(devices),
+                                          _device_shares(groups, devices, wg if len(devices) > 1 else 0))]
     for th in threads:
         th.start()
     for th in threads:

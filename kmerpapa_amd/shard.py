@@ -129,20 +129,21 @@ def sharded_run_groups(run_groups, rank, world, all_gather, devices=None, width=
     """
     fixed = devices
 
-    def _width(gen_pat, M, max_block):
+    def _width(gen_pat, itype, max_block):
         if width is not None:
             return width
         from . import engine
-        return engine.shard_width(gen_pat, engine.counts_itype(M), max_block)
+        return engine.shard_width(gen_pat, itype, max_block)
 
-    def prepare(gen_pat, groups, devices=None, max_block=0):
+    def prepare(gen_pat, groups, devices=None, max_block=0, itype=np.uint32):
         inner = getattr(run_groups, "prepare", None)
-        mine = rank_groups(groups, rank, world, _width(gen_pat, None, max_block))
+        mine = rank_groups(groups, rank, world, _width(gen_pat, itype, max_block))
         if inner is not None and mine:
-            inner(gen_pat, mine, devices=fixed if fixed is not None else devices, max_block=max_block)
+            inner(gen_pat, mine, devices=fixed if fixed is not None else devices, max_block=max_block, itype=itype)
 
     def run(gen_pat, M, U, groups, devices=None, max_block=0):
-        w = _width(gen_pat, M, max_block)
+        from . import engine
+        w = _width(gen_pat, engine.counts_itype(M), max_block)
         mine = rank_groups(groups, rank, world, w)
         if mine:
             rt, re, nl = run_groups(gen_pat, M, U, mine, devices=fixed if fixed is not None else devices,

@@ -188,7 +188,7 @@ def test_cv_driver_prepares_devices_during_fold_split():
     def run(gen_pat, M, U, groups, devices=None, max_block=0):
         return E.run_groups(gen_pat, M, U, groups, devices=devices, max_block=max_block)
 
-    def prepare(gen_pat, groups, devices=None, max_block=0):
+    def prepare(gen_pat, groups, devices=None, max_block=0, itype=np.uint32):
         seen.append((gen_pat, [(g[0], g[1], list(g[3])) for g in groups]))
     run.prepare = prepare
     ref = cvm.cv_roots(c["gen_pat"], ctx, c["alphas"], c["penalties"], c["nfolds"], c["seed"], 1, np.uint32,
@@ -209,7 +209,7 @@ def test_cv_driver_prepare_errors_surface():
     def run(gen_pat, M, U, groups, devices=None, max_block=0):
         return E.run_groups(gen_pat, M, U, groups, devices=devices, max_block=max_block)
 
-    def prepare(gen_pat, groups, devices=None, max_block=0):
+    def prepare(gen_pat, groups, devices=None, max_block=0, itype=np.uint32):
         raise MemoryError("lattice does not fit")
     run.prepare = prepare
     with pytest.raises(MemoryError):
@@ -400,3 +400,47 @@ def test_prepare_groups_surfaces_plan_errors(monkeypatch):
     with pytest.raises(engine.KPError) as e:
         engine.prepare_groups("NNMNN", groups, devices=[0, 1])
     assert e.value.code == -2
+
+
+def test_prepared_shares_at_the_counts_width(monkeypatch):
+    """The CV driver's prepare hook gets the counts' width, and the shares it prepares are the
+    ones run_groups will run: with 64-bit counts the 9-mer lattice's workgroup holds 4 lanes
+    (engine.shard_width), so whole 4-lane pieces are dealt and a pass holds at most 5 lanes;
+    the sharded wrapper (torchrun ranks) hands the same width and itype to the inner hook."""
+    from kmerpapa_amd import engine
+    gp = "NNNNMNNNN"
+    assert engine.shard_width(gp, np.uint32) == 5 and engine.shard_width(gp, np.uint64) == 4
+    groups = [(f, a, 1.0, [3.0, 4.0, 5.0, 6.0, 7.0]) for a in (0.5, 1.0, 2.0, 5.0, 10.0) for f in shard.fold_order(5)]
+    reserved = {}
+
+    class Plan:
+        info = {"lanes_per_workgroup": 5}  # (the plan's width before counts: uint32)
+
+        def __init__(self, dev):
+            self.dev = dev
+
+        def require_lanes(self, n=1):
+            return 9
+
+        def reserve(self, lanes):
+            reserved[self.dev] = lanes
+    monkeypatch.setattr(engine, "get_plan", lambda dev, gp, mb=0, replica=0: Plan(dev))
+    for itype, width in ((np.uint32, 5), (np.uint64, 4)):
+        reserved.clear()
+        engine.prepare_groups(gp, groups, devices=list(range(8)), itype=itype)
+        for d in range(8):
+            mine = shard.rank_groups(groups, d, 8, width)
+            passes, _ = engine.plan_passes(mine, engine.pass_cap(mine, 9, width), width)
+            assert reserved[d] == max(sum(len(g[3]) for g in p) for p in passes) <= width + 1
+    seen = []
+
+    def inner(*a, **k):
+        raise AssertionError("not run")
+
+    def inner_prepare(gen_pat, grps, devices=None, max_block=0, itype=np.uint32):
+        seen.append((grps, itype))
+    inner.prepare = inner_prepare
+    for r in (0, 7):
+        run = shard.sharded_run_groups(inner, r, 8, all_gather=None)
+        run.prepare(gp, groups, itype=np.uint64)
+        assert seen[-1] == (shard.rank_groups(groups, r, 8, 4), np.uint64)
